@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""bench.py -- throughput of the SDF sphere-tracing hot path on MI355X.
+
+One step = one frame of BASELINE.json's workload (default C4: the 8-primitive
+smooth-min CSG scene with soft shadows, 5-tap AO and tetrahedral normals at
+3840x2160, 128 max steps), rendered by the HIP kernel through the C-ABI
+(sdf_render).  With N ranks (one process per GPU, torchrun) each rank renders
+its interleaved 8-row blocks of the frame and the blocks are gathered to rank 0
+over RCCL and scattered into the frame (sdf_deinterleave); the gather of
+frame i overlaps the render of frame i+1 (double-buffered).  Total work per
+step is one frame whatever N is ("scaling": "strong").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
+                    [--precision fast|exact] [--no-cpu-baseline]
+
+Prints ONE JSON line (rank 0).  `value` = frame pixels x K / max-over-ranks
+wall time of the K timed steps, in Mpixels/s.  `roofline` is the render
+kernel's achieved algorithmic FP32 rate (SURVEY.md 8(d) counting rule,
+per-pixel step counts from the CPU oracle's full-frame statistics in
+tests/golden/stats_<cfg>_p0.npz) over the kernel's average duration measured
+with HIP events on the launch stream, against the 157.3 TFLOP/s FP32 vector
+peak.  `cpu_baseline` times the CPU oracle (a restatement of the reference
+shader: the reference's own OpenCL kernel is empty and no CPU OpenCL device
+exists) on a bounded sample of the same frame, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Mpixels/s (primary+shadow+AO) at 3840×2160, 1/2/4/8 MI355X"
+FP32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 vector (packed) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--precision", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--pose", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-stride", type=int, default=4,
+                    help="CPU baseline renders every k-th 8-row block of the frame")
+    ap.add_argument("--cpu-frames", type=int, default=5)
+    return ap.parse_args()
+
+
+def rank_flops(frame, tiling, pose):
+    """Algorithmic flops of one render launch over the rows `tiling` owns."""
+    from sdf3d_amd import costmodel
+    path = ROOT / "tests" / "golden" / f"stats_{frame.name}_p{pose}.npz"
+    if not path.exists() or frame.scene.kind != 0:
+        return None
+    z = np.load(path)
+    if int(z["width"]) != frame.params.width or int(z["height"]) != frame.params.height:
+        return None
+    H, B = frame.params.height, tiling.block_rows
+    ys = [y for y in range(H) if (y // B) >= tiling.first_block
+          and ((y // B) - tiling.first_block) % tiling.block_stride == 0]
+    c = costmodel.coefficients(frame)
+    return c.flops(len(ys) * frame.params.width, z["row_sp"][ys].sum(), z["row_ss"][ys].sum())
+
+
+def pmc_traffic(cfg, precision):
+    """HBM bytes per render launch from a committed rocprofv3 PMC summary
+    (profiles/pmc_<cfg>_<precision>.json, written by tools/pmc_traffic.py), or None."""
+    p = ROOT / "profiles" / f"pmc_{cfg}_{precision}.json"
+    if not p.exists():
+        return None
+    try:
+        return float(json.loads(p.read_text())["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(frame, stride, frames):
+    import oracle
+    from sdf3d_amd import renderer as R
+    t = R.tiling(0, stride, 8)
+    n = oracle.default_threads()
+    rows = oracle.owned_rows(frame.params.height, t)
+    oracle.render(frame, t, nthreads=n)          # warm-up
+    times = []
+    for _ in range(frames):
+        t0 = time.perf_counter()
+        oracle.render(frame, t, nthreads=n)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    px = rows * frame.params.width
+    return {"value": round(px / med / 1e6, 4), "unit": "Mpixels/s", "cores": n, "kind": "port",
+            "sample": f"{frame.name} {frame.params.width}x{frame.params.height}, every "
+                      f"{stride}th 8-row block ({rows} rows, {px} px), median of {frames} "
+                      f"after 1 warm-up, {n} OpenMP threads, CPU oracle "
+                      f"(oracle/oracle_core.h, -O3 -ffp-contract=off)",
+            "seconds_per_sample": round(med, 3)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            sys.exit(f"--gpus {args.gpus} needs torchrun --nproc-per-node {args.gpus}")
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+    import torch.distributed as dist
+    from sdf3d_amd import Renderer, abi, scenes
+    from sdf3d_amd import renderer as R
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    prec = abi.PRECISION_FAST if args.precision == "fast" else abi.PRECISION_EXACT
+    frame = scenes.config(args.config, precision=prec, pose=args.pose)
+    W, H = frame.params.width, frame.params.height
+    rd = Renderer(dev)
+    t = R.tiling(rank, world, 8)
+    rows = R.owned_rows(H, t)
+    stride = R.owned_rows(H, R.tiling(0, world, 8))   # rank 0 owns the most rows
+    stream = torch.cuda.current_stream(dev)
+
+    nbuf = 2 if world > 1 else 1
+    local = [torch.empty((stride, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    if world > 1 and rank == 0:
+        gathered = [torch.empty((world * stride, W, 4), dtype=torch.float32, device=dev)
+                    for _ in range(nbuf)]
+        frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+                      for _ in range(nbuf)]
+        side = torch.cuda.Stream(device=dev)
+        deint_done = [None] * nbuf
+    works = [None] * nbuf
+
+    k_steps = args.steps + args.warmup
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
+
+    def step(i):
+        b = i % nbuf
+        if world > 1 and works[b] is not None:
+            works[b].wait()                   # gather i-2 has finished reading local[b]
+        ev0[i].record(stream)
+        rd.render(frame, t, out=local[b][:rows], stream=stream)
+        ev1[i].record(stream)
+        if world > 1:
+            if rank == 0:
+                if deint_done[b] is not None:
+                    stream.wait_event(deint_done[b])  # deinterleave i-2 has read gathered[b]
+                glist = [gathered[b][r * stride:(r + 1) * stride] for r in range(world)]
+                works[b] = dist.gather(local[b], gather_list=glist, dst=0, async_op=True)
+                with torch.cuda.stream(side):
+                    works[b].wait()
+                    rd.deinterleave(gathered[b], world, stride, W, H, 8, out=frames_out[b],
+                                    stream=side)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    deint_done[b] = ev
+            else:
+                works[b] = dist.gather(local[b], gather_list=None, dst=0, async_op=True)
+
+    def drain():
+        for w in works:
+            if w is not None:
+                w.wait()
+        torch.cuda.synchronize(dev)
+
+    log(f"[bench] rank {rank}/{world} {args.config} {W}x{H} rows={rows} "
+        f"precision={args.precision} warmup={args.warmup} steps={args.steps}")
+    for i in range(args.warmup):
+        step(i)
+    drain()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, k_steps):
+        step(i)
+    drain()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    kernel_ms = [ev0[i].elapsed_time(ev1[i]) for i in range(args.warmup, k_steps)]
+    kavg_ms = sum(kernel_ms) / len(kernel_ms)
+    flops = rank_flops(frame, t, args.pose)
+
+    if rank == 0:
+        value = W * H * args.steps / elapsed / 1e6
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mpixels/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {frame.meta['description']}",
+                       "width": W, "height": H, "max_steps": frame.params.max_steps,
+                       "precision": args.precision, "pose": args.pose,
+                       "tiling": "8-row interleaved blocks" if world > 1 else "whole frame",
+                       "gather": "RCCL gather to rank 0 + sdf_deinterleave" if world > 1
+                       else None},
+            "fps": round(args.steps / elapsed, 2),
+            "kernel_ms": round(kavg_ms, 4),
+        }
+        if flops is not None:
+            ach = flops / (kavg_ms * 1e-3) / 1e12
+            traffic = pmc_traffic(args.config, args.precision) if world == 1 else None
+            out["roofline"] = {"bound": "valu", "achieved": round(ach, 2),
+                               "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                               "flops_per_launch": flops,
+                               "store_GBps": round(rows * W * 16 / (kavg_ms * 1e-3) / 1e9, 1)}
+        else:
+            out["roofline"] = None
+        if world == 1 and not args.no_cpu_baseline:
+            log("[bench] cpu baseline ...")
+            out["cpu_baseline"] = cpu_baseline(frame, args.cpu_sample_stride, args.cpu_frames)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

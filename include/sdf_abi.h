@@ -1,0 +1,236 @@
+/*
+ * sdf_abi.h -- C-ABI of the MI355X-native SDF sphere-tracing renderer.
+ *
+ * This is the drop-in boundary that replaces the reference's device programs
+ * (ezorzin/SDF3D `Code/shader/voxel_fragment.frag`, `voxel_geometry.geom`,
+ * `voxel_vertex.vert` and the never-enqueued `Code/kernel/thekernel_1.cl`).
+ * Plain C: POD structs, plain pointers and sizes, integer status codes.  No
+ * torch / C++ types cross this boundary.
+ *
+ * Reference interface each entry point replaces (paths relative to the
+ * reference root):
+ *
+ *   sdf_defaults()   the hard-coded constants and scene of the fragment shader:
+ *                    voxel_fragment.frag:15-23 (PI, MAX_STEPS, MAX_DISTANCE,
+ *                    EPSILON), :54-81 (sphere + plane, hard union), :178-189
+ *                    (camera, light, material), :205 (shadow k = 10); and the
+ *                    host's default window / view (main.cpp:4-11: 800x600,
+ *                    orbit and pan at 0 -> V_mat = identity).
+ *   sdf_render()     one frame of `gl->plot(sh, proj_mode)` (main.cpp:95), i.e.
+ *                    the fragment stage `main()` (voxel_fragment.frag:160-211)
+ *                    run once per pixel, with the pixel -> `quad` mapping of
+ *                    voxel_geometry.geom:26-52 folded into the index math, and
+ *                    with the uniforms `V_mat`, `AR` (voxel_fragment.frag:5-7)
+ *                    passed explicitly in sdf_camera.  The output is the
+ *                    shader's `fragment_color` (:12, :210) as float RGBA.
+ *   sdf_deinterleave() gathers per-device row blocks into one frame (new: the
+ *                    reference has a single GL context, main.cpp:48,53).
+ *   sdf_strerror()   error text (the reference has none: main.cpp:109).
+ *
+ * Conventions
+ *   - Framebuffer: width x height pixels, 4 floats (R,G,B,A) per pixel,
+ *     row-major, row 0 = BOTTOM row (GL window origin), pixel (x, y) at
+ *     rgba[(y * width + x) * 4].
+ *   - Matrices: 16 floats, column-major, exactly like a GLSL mat4 uniform.
+ *   - All device pointers are HIP device pointers on the current device; the
+ *     call is asynchronous on `stream` (a hipStream_t, NULL = null stream).
+ *   - Functions return SDF_OK (0) or a negative SDF_E* code; they never throw.
+ */
+#ifndef SDF_ABI_H
+#define SDF_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDF_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define SDF_OK               0
+#define SDF_E_INVALID_ARG   -1  /* null pointer, bad size, bad enum value      */
+#define SDF_E_UNSUPPORTED   -2  /* valid request this build cannot serve       */
+#define SDF_E_HIP           -3  /* a HIP runtime call failed                   */
+#define SDF_E_NO_DEVICE     -4  /* no gfx950 device visible                    */
+
+/* ---- scene description -------------------------------------------------- */
+#define SDF_MAX_PRIMS 16
+
+/* Primitive kinds.  Parameter layout in sdf_primitive.p[]:
+ *   SPHERE     c.xyz, radius                       (voxel_fragment.frag:54-64)
+ *   PLANE      n.xyz, h        sdf = dot(p, n) + h   (voxel_fragment.frag:66-71
+ *                              is n = (0,1,0), h = 0: sdf = p.y)
+ *   BOX        c.xyz, half.xyz                     (extension, parity unpinned)
+ *   ROUND_BOX  c.xyz, half.xyz, r                  (extension)
+ *   TORUS      c.xyz, R, r     ring in the xz plane (extension)
+ *   CAPSULE    a.xyz, b.xyz, r                     (extension)
+ *   CYLINDER   c.xyz, r, half_height, y-axis, capped (extension)            */
+typedef enum {
+  SDF_PRIM_SPHERE = 0,
+  SDF_PRIM_PLANE = 1,
+  SDF_PRIM_BOX = 2,
+  SDF_PRIM_ROUND_BOX = 3,
+  SDF_PRIM_TORUS = 4,
+  SDF_PRIM_CAPSULE = 5,
+  SDF_PRIM_CYLINDER = 6,
+  SDF_PRIM_KIND_COUNT = 7
+} sdf_prim_kind;
+
+/* How primitive i combines with the running scene distance d (d starts at
+ * +INF, voxel_fragment.frag:75).  UNION is GLSL `min(d, s)` exactly as
+ * voxel_fragment.frag:77-78; the smooth forms use the polynomial smooth-min
+ * with blend radius `k` (extension, see DESIGN.md "Scene spec").            */
+typedef enum {
+  SDF_OP_UNION = 0,
+  SDF_OP_SMOOTH_UNION = 1,
+  SDF_OP_SUBTRACT = 2,         /* max(d, -s)                                  */
+  SDF_OP_INTERSECT = 3,        /* max(d, s)                                   */
+  SDF_OP_SMOOTH_SUBTRACT = 4,
+  SDF_OP_SMOOTH_INTERSECT = 5,
+  SDF_OP_COUNT = 6
+} sdf_csg_op;
+
+typedef struct {
+  int32_t kind;   /* sdf_prim_kind */
+  int32_t op;     /* sdf_csg_op    */
+  float k;        /* smooth blend radius (> 0 for SMOOTH_* ops)               */
+  float reserved;
+  float p[12];    /* kind-specific parameters, see above                      */
+} sdf_primitive;  /* 64 bytes */
+
+typedef enum {
+  SDF_SCENE_PRIMITIVES = 0,    /* CSG list of prims[0..count)                 */
+  SDF_SCENE_MANDELBULB = 1     /* power-8 Mandelbulb distance estimator        */
+} sdf_scene_kind;
+
+typedef struct {
+  int32_t kind;                /* sdf_scene_kind                               */
+  int32_t count;               /* number of primitives used (PRIMITIVES)       */
+  sdf_primitive prims[SDF_MAX_PRIMS];
+  /* MANDELBULB: world p -> local q = (p - center) / scale, DE(q) * scale.   */
+  float bulb_center[3];
+  float bulb_scale;
+  int32_t bulb_iterations;     /* default 12                                   */
+  float bulb_bailout;          /* default 2                                    */
+  int32_t reserved[2];
+} sdf_scene;
+
+/* Camera: voxel_fragment.frag:26-30, :178-180, :191-192.                    */
+typedef struct {
+  float view[16];              /* V_mat uniform, column-major                  */
+  float eye[3];                /* camera.pos before inverse(V_mat): (0,0.2,2)  */
+  float fov_deg;               /* camera.fov = 60                              */
+  float aspect;                /* AR uniform; <= 0 means width / height        */
+  float pi;                    /* the shader's PI literal 3.1415925359f (a1)   */
+} sdf_camera;
+
+/* Light: voxel_fragment.frag:32-40, :182-184.                               */
+typedef struct {
+  float pos[3];                /* (5, 5, 0)                                    */
+  float ambient;               /* light.amb = 0.1                              */
+  float color[3];              /* light.col = 0.7: declared, never used (:183) */
+  float reserved;
+} sdf_light;
+
+/* Material: voxel_fragment.frag:42-49, :186-189.                            */
+typedef struct {
+  float amb[3];                /* (0, 0.2, 0.8)                                */
+  float dif[3];                /* (0, 0.2, 0.8)                                */
+  float ref[3];                /* (0.5, 0.5, 0.5)                              */
+  float shininess;             /* 12                                           */
+} sdf_material;
+
+/* Render flags */
+#define SDF_FLAG_SHADOW     0x1  /* soft shadow march (voxel_fragment.frag:205) */
+#define SDF_FLAG_AO         0x2  /* ambient occlusion (extension)               */
+
+typedef enum {
+  SDF_NORMAL_CENTRAL = 0,      /* 6-tap central differences (:134-155)         */
+  SDF_NORMAL_TETRA = 1         /* 4-tap tetrahedral differences (extension)    */
+} sdf_normal_mode;
+
+typedef enum {
+  SDF_PRECISION_EXACT = 0,     /* IEEE div/sqrt, no FMA contraction: bit-level
+                                  restatement of the shader arithmetic         */
+  SDF_PRECISION_FAST = 1       /* hardware sqrt/rcp, FMA contraction           */
+} sdf_precision;
+
+typedef struct {
+  int32_t width, height;       /* framebuffer size (main.cpp:4-5: 800 x 600)   */
+  int32_t max_steps;           /* MAX_STEPS = 100 (both marches, :17)          */
+  float max_dist;              /* MAX_DISTANCE = 100 (:18)                     */
+  float eps;                   /* EPSILON = 0.01 (:19)                         */
+  float shadow_k;              /* 10 (:205)                                    */
+  float normal_eps;            /* DX/DY/DZ offset = EPSILON (:21-23)           */
+  float shadow_offset;         /* P + N*2*EPSILON: 2 (:205)                    */
+  int32_t flags;               /* SDF_FLAG_*; reference = SDF_FLAG_SHADOW      */
+  int32_t normal_mode;         /* sdf_normal_mode; reference = CENTRAL          */
+  int32_t ao_taps;             /* AO samples (5 when SDF_FLAG_AO)              */
+  float ao_step;               /* AO: h_i = ao_base + ao_step * i / (taps-1)   */
+  float ao_base;
+  float ao_falloff;            /* per-tap weight decay                         */
+  float ao_strength;           /* ao = clamp(1 - strength * occ, 0, 1)         */
+  int32_t precision;           /* sdf_precision                                */
+  int32_t reserved[4];
+} sdf_params;
+
+/* Which rows of the frame a call renders.  Rows are grouped into blocks of
+ * `block_rows` rows; block b (rows [b*block_rows, (b+1)*block_rows)) is
+ * rendered iff b >= first_block and (b - first_block) % block_stride == 0.
+ * Rendered rows are written densely ("packed") in increasing y order, so
+ * {block_rows = 8, first_block = r, block_stride = N} is device r's share
+ * of an N-device interleaved tiling and {8, 0, 1} is the whole frame.        */
+typedef struct {
+  int32_t block_rows;
+  int32_t first_block;
+  int32_t block_stride;
+  int32_t reserved;
+} sdf_tiling;
+
+/* ---- entry points -------------------------------------------------------- */
+
+/* ABI version of the loaded library (== SDF_ABI_VERSION when compatible). */
+int sdf_abi_version(void);
+
+/* Fill every non-null struct with the reference defaults (see top comment).
+ * `width`/`height` set params->width/height (<= 0: 800 x 600, main.cpp:4-5). */
+int sdf_defaults(sdf_scene* scene, sdf_camera* camera, sdf_light* light,
+                 sdf_material* material, sdf_params* params,
+                 int32_t width, int32_t height);
+
+/* Validate a request without touching the device. */
+int sdf_validate(const sdf_scene* scene, const sdf_camera* camera,
+                 const sdf_light* light, const sdf_material* material,
+                 const sdf_params* params, const sdf_tiling* tiling);
+
+/* Number of rows a tiling owns in a frame of `height` rows (>= 0), or a
+ * negative SDF_E* code. */
+int sdf_owned_rows(int32_t height, const sdf_tiling* tiling);
+
+/* Render the rows owned by `tiling` (NULL = whole frame) into `rgba`
+ * (device, owned_rows * width * 4 floats, packed as described above).
+ * `steps` (device, may be NULL) receives 2 int32 per pixel: the primary and
+ * the shadow march iteration counts (diagnostics / flop accounting).
+ * Asynchronous on `stream`. */
+int sdf_render(const sdf_scene* scene, const sdf_camera* camera,
+               const sdf_light* light, const sdf_material* material,
+               const sdf_params* params, const sdf_tiling* tiling,
+               float* rgba, int32_t* steps, void* stream);
+
+/* Scatter `nparts` packed row-block buffers (part r = rank r's output for
+ * tiling {block_rows, r, nparts}), laid out back to back in `parts` with a
+ * pitch of `part_stride_rows` rows each, into the full frame `frame`
+ * (height * width * 4 floats).  Device pointers; asynchronous on `stream`. */
+int sdf_deinterleave(const float* parts, int32_t nparts,
+                     int32_t part_stride_rows, int32_t width, int32_t height,
+                     int32_t block_rows, float* frame, void* stream);
+
+/* Short description of a status code. */
+const char* sdf_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SDF_ABI_H */

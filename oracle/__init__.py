@@ -1,0 +1,151 @@
+"""CPU oracle for the SDF hot path -- TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper over oracle/build/liboracle.so, the plain-C restatement of the
+reference fragment shader (/root/reference/Code/shader/voxel_fragment.frag;
+see oracle/oracle_core.h for the line-by-line mapping and the parity status:
+pinned by analytic known-answer tests only, "parity unpinned" against
+reference-produced outputs, because the GLSL reference cannot run here).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this package, and only as the checker / CPU baseline.  The product path
+(sdf3d_amd, libsdf3d.so) never imports or calls it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from sdf3d_amd import abi  # struct layouts of include/sdf_abi.h (types only)
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "liboracle.so"
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        build()
+    lib = C.CDLL(str(LIB_PATH))
+    P = C.POINTER
+    frame_args = [P(abi.sdf_scene), P(abi.sdf_camera), P(abi.sdf_light), P(abi.sdf_material),
+                  P(abi.sdf_params)]
+    lib.sdf_oracle_defaults.argtypes = frame_args + [C.c_int, C.c_int]
+    lib.sdf_oracle_defaults.restype = C.c_int
+    for fn in (lib.sdf_oracle_render, lib.sdf_oracle_render_f64):
+        fn.argtypes = frame_args + [P(abi.sdf_tiling), C.c_void_p, C.c_void_p, C.c_int]
+        fn.restype = C.c_int
+    lib.sdf_oracle_owned_rows.argtypes = [C.c_int, P(abi.sdf_tiling)]
+    lib.sdf_oracle_owned_rows.restype = C.c_int
+    lib.sdf_oracle_scene_sdf.argtypes = [P(abi.sdf_scene), C.c_float, C.c_float, C.c_float]
+    lib.sdf_oracle_scene_sdf.restype = C.c_float
+    lib.sdf_oracle_uniforms.argtypes = [P(abi.sdf_camera), P(abi.sdf_params), C.c_void_p]
+    lib.sdf_oracle_uniforms.restype = C.c_int
+    F3 = C.POINTER(C.c_float)
+    lib.sdf_oracle_raymarch.argtypes = [P(abi.sdf_scene), P(abi.sdf_params), F3, F3,
+                                        P(C.c_int)]
+    lib.sdf_oracle_raymarch.restype = C.c_float
+    lib.sdf_oracle_shadow.argtypes = [P(abi.sdf_scene), P(abi.sdf_params), F3, F3, C.c_float,
+                                      P(C.c_int)]
+    lib.sdf_oracle_shadow.restype = C.c_float
+    lib.sdf_oracle_normal.argtypes = [P(abi.sdf_scene), P(abi.sdf_params), F3, F3]
+    lib.sdf_oracle_normal.restype = None
+    _lib = lib
+    return lib
+
+
+def _f3(v):
+    return (C.c_float * 3)(*[float(x) for x in v])
+
+
+def raymarch(scene, params, pos, direction):
+    """(distance, steps) of the fp32 raymarch (voxel_fragment.frag:86-103)."""
+    n = C.c_int(0)
+    d = load().sdf_oracle_raymarch(C.byref(scene), C.byref(params), _f3(pos), _f3(direction),
+                                   C.byref(n))
+    return float(d), n.value
+
+
+def shadow(scene, params, pos, direction, k=10.0):
+    """(shadow, steps) of the fp32 soft shadow (voxel_fragment.frag:105-132)."""
+    n = C.c_int(0)
+    s = load().sdf_oracle_shadow(C.byref(scene), C.byref(params), _f3(pos), _f3(direction),
+                                 float(k), C.byref(n))
+    return float(s), n.value
+
+
+def normal(scene, params, pos):
+    out = (C.c_float * 3)()
+    load().sdf_oracle_normal(C.byref(scene), C.byref(params), _f3(pos), out)
+    return np.array(list(out), dtype=np.float32)
+
+
+def default_threads() -> int:
+    n = os.environ.get("OMP_NUM_THREADS")
+    if n and n.isdigit():
+        return max(1, int(n))
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def defaults(width: int = 800, height: int = 600):
+    """The oracle's own statement of the reference defaults (5 structs)."""
+    s, c, l, m, p = (abi.sdf_scene(), abi.sdf_camera(), abi.sdf_light(), abi.sdf_material(),
+                     abi.sdf_params())
+    rc = load().sdf_oracle_defaults(C.byref(s), C.byref(c), C.byref(l), C.byref(m), C.byref(p),
+                                    width, height)
+    assert rc == 0
+    return s, c, l, m, p
+
+
+def owned_rows(height: int, t=None) -> int:
+    if t is None:
+        return height
+    return load().sdf_oracle_owned_rows(height, C.byref(t))
+
+
+def render(frame, t=None, nthreads: int | None = None, twin: bool = False):
+    """Render `frame` (sdf3d_amd.scenes.Frame) on the CPU.
+
+    Returns (rgba float32 [rows, W, 4], steps int32 [rows, W, 2]).
+    `twin=True` runs the fp64 twin (diagnosis only)."""
+    lib = load()
+    p = frame.params
+    rows = owned_rows(p.height, t)
+    rgba = np.empty((rows, p.width, 4), dtype=np.float32)
+    steps = np.empty((rows, p.width, 2), dtype=np.int32)
+    fn = lib.sdf_oracle_render_f64 if twin else lib.sdf_oracle_render
+    rc = fn(C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
+            C.byref(frame.material), C.byref(frame.params),
+            C.byref(t) if t is not None else None,
+            rgba.ctypes.data_as(C.c_void_p), steps.ctypes.data_as(C.c_void_p),
+            nthreads if nthreads is not None else default_threads())
+    if rc != 0:
+        raise RuntimeError(f"oracle render failed: {rc}")
+    return rgba, steps
+
+
+def scene_sdf(scene, x: float, y: float, z: float) -> float:
+    return float(load().sdf_oracle_scene_sdf(C.byref(scene), x, y, z))
+
+
+def uniforms(camera, params) -> dict:
+    out = np.zeros(21, dtype=np.float32)
+    rc = load().sdf_oracle_uniforms(C.byref(camera), C.byref(params),
+                                    out.ctypes.data_as(C.c_void_p))
+    assert rc == 0
+    return {"inv_view": out[:16].copy(), "cam": out[16:19].copy(), "focal": float(out[19]),
+            "aspect": float(out[20])}

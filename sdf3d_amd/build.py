@@ -1,0 +1,86 @@
+"""Build the HIP C-ABI library ``sdf3d_amd/lib/libsdf3d.so`` for gfx950.
+
+Explicit ``hipcc`` invocations (no JIT, no torch extension cache) so the built
+library lives in-tree and travels to the GPU box with the repository snapshot.
+
+Translation units:
+  render_exact.hip  -- render kernel, -ffp-contract=off, IEEE div/sqrt
+  render_fast.hip   -- render kernel, FMA contraction, hardware sqrt/rcp
+  deinterleave.hip  -- multi-device row-block scatter
+  sdf_abi.cpp       -- the extern "C" entry points of include/sdf_abi.h
+
+Run ``python -m sdf3d_amd.build`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "build"
+LIB_DIR = PKG / "lib"
+LIB = LIB_DIR / "libsdf3d.so"
+ARCH = os.environ.get("SDF3D_ARCH", "gfx950")
+
+COMMON = ["-O3", "-fPIC", "-std=c++17", "-Wall", f"--offload-arch={ARCH}"]
+UNITS = [
+    ("render_exact.hip", ["-ffp-contract=off"]),
+    ("render_fast.hip", ["-ffp-contract=fast"]),
+    ("deinterleave.hip", []),
+    ("sdf_abi.cpp", ["-ffp-contract=off", "-x", "hip"]),
+]
+HEADERS = [CSRC / "kernel_args.h", CSRC / "render_kernel.inc", ROOT / "include" / "sdf_abi.h"]
+
+
+def _hipcc() -> str:
+    exe = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not Path(exe).exists():
+        raise RuntimeError("hipcc not found: the HIP library cannot be built")
+    return exe
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(str(c) for c in cmd), flush=True)
+    subprocess.run([str(c) for c in cmd], check=True)
+
+
+def build_library(force: bool = False, verbose: bool = True) -> Path:
+    hipcc = _hipcc()
+    OBJ.mkdir(parents=True, exist_ok=True)
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    objs = []
+    for src, extra in UNITS:
+        s = CSRC / src
+        o = OBJ / (s.stem + ".o")
+        objs.append(o)
+        if force or _stale(o, [s, *HEADERS, Path(__file__)]):
+            _run([hipcc, *COMMON, *extra, "-c", s, "-o", o], verbose)
+    if force or _stale(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], verbose)
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(verbose: bool = True) -> Path:
+    """Compile the CPU oracle (test infrastructure) with its own Makefile."""
+    _run(["make", "-s", "-C", ROOT / "oracle"], verbose)
+    return ROOT / "oracle" / "build" / "liboracle.so"
+
+
+if __name__ == "__main__":
+    build_library(force="--force" in sys.argv)
+    build_oracle()

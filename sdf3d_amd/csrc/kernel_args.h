@@ -1,0 +1,60 @@
+// kernel_args.h -- uniform block handed from the C-ABI host code to the HIP
+// render kernels.  Everything here is per-frame constant: the host hoists the
+// shader's uniform-only work (inverse(V_mat) twice per pixel, camera.pos, the
+// focal term -2/tan(fov*PI/360); voxel_fragment.frag:180, :191-192) so each
+// lane only does per-pixel arithmetic.  Passed by value as the kernel argument
+// so the fields are read with scalar loads (SGPRs), never per lane.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/sdf_abi.h"
+
+namespace sdf {
+
+struct KernelArgs {
+  // camera (hoisted uniforms)
+  float inv_view[16];   // inverse(V_mat), column-major
+  float cam[3];         // (inverse(V_mat) * vec4(camera.pos, 1)).xyz
+  float focal;          // -2 / tan(fov * PI / 360)
+  float aspect;         // AR
+  // light + material (voxel_fragment.frag:182-189)
+  float light_pos[3];
+  float light_amb;
+  float mat_amb[3];
+  float mat_dif[3];
+  float mat_ref[3];
+  float shininess;
+  // march parameters
+  int32_t width, height;
+  int32_t max_steps;
+  float max_dist, eps, shadow_k, normal_eps, shadow_offset;
+  int32_t flags, normal_mode;
+  int32_t ao_taps;
+  float ao_step, ao_base, ao_falloff, ao_strength;
+  // tiling
+  int32_t block_rows, first_block, block_stride, rows;
+  // scene
+  int32_t scene_kind, prim_count;
+  float bulb_center[3], bulb_scale, bulb_bail2;
+  int32_t bulb_iterations;
+  sdf_primitive prims[SDF_MAX_PRIMS];
+  // outputs
+  float* rgba;          // rows * width float4, packed rows
+  int32_t* steps;       // rows * width int2 or null
+};
+
+// Kernel launchers, one per precision translation unit (render_exact.hip /
+// render_fast.hip); `variant` selects a compile-time scene specialisation
+// (see render_kernel.inc).  Return a hipError_t as int.
+int launch_render_exact(const KernelArgs& a, int variant, void* stream);
+int launch_render_fast(const KernelArgs& a, int variant, void* stream);
+int launch_deinterleave(const float* parts, int nparts, int part_stride_rows, int width,
+                        int height, int block_rows, float* frame, void* stream);
+
+// Compile-time scene variants the dispatcher can pick (0 = generic list).
+enum SceneVariant : int {
+  kVariantGeneric = 0,
+};
+
+}  // namespace sdf

@@ -1,0 +1,312 @@
+// sdf_abi.cpp -- host side of the C-ABI declared in include/sdf_abi.h.
+//
+// Replaces what the reference does around `gl->plot(sh, proj_mode)`
+// (/root/reference/Code/src/main.cpp:95): it takes the per-frame uniforms
+// (the shader's V_mat and AR, voxel_fragment.frag:5-7) plus the scene, light
+// and material that the reference hard-codes in the shader
+// (voxel_fragment.frag:178-189), hoists the uniform-only arithmetic the shader
+// repeats per pixel (inverse(V_mat) at :180 and :192, camera.pos at :180, the
+// focal term at :191), and launches one HIP kernel over the requested rows.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../include/sdf_abi.h"
+#include "kernel_args.h"
+
+// Layout contract with the ctypes mirror (sdf3d_amd/abi.py STRUCT_SIZES).
+static_assert(sizeof(sdf_primitive) == 64, "sdf_primitive layout");
+static_assert(sizeof(sdf_scene) == 8 + 64 * SDF_MAX_PRIMS + 32, "sdf_scene layout");
+static_assert(sizeof(sdf_camera) == 88, "sdf_camera layout");
+static_assert(sizeof(sdf_light) == 32, "sdf_light layout");
+static_assert(sizeof(sdf_material) == 40, "sdf_material layout");
+static_assert(sizeof(sdf_params) == 80, "sdf_params layout");
+static_assert(sizeof(sdf_tiling) == 16, "sdf_tiling layout");
+
+namespace {
+
+// Inverse of a column-major 4x4 matrix via 2x2 sub-determinants, in double,
+// rounded once to float.  GLSL's inverse() precision is unspecified; this is
+// the correctly rounded exact inverse for all but pathological inputs.
+bool invert_view(const float* mf, float* out) {
+  double m[16];
+  for (int i = 0; i < 16; ++i) m[i] = mf[i];
+  // element (row r, col c) of a column-major matrix is m[c*4 + r]
+  auto e = [&](int r, int c) { return m[c * 4 + r]; };
+  const double s0 = e(0, 0) * e(1, 1) - e(1, 0) * e(0, 1);
+  const double s1 = e(0, 0) * e(1, 2) - e(1, 0) * e(0, 2);
+  const double s2 = e(0, 0) * e(1, 3) - e(1, 0) * e(0, 3);
+  const double s3 = e(0, 1) * e(1, 2) - e(1, 1) * e(0, 2);
+  const double s4 = e(0, 1) * e(1, 3) - e(1, 1) * e(0, 3);
+  const double s5 = e(0, 2) * e(1, 3) - e(1, 2) * e(0, 3);
+  const double c5 = e(2, 2) * e(3, 3) - e(3, 2) * e(2, 3);
+  const double c4 = e(2, 1) * e(3, 3) - e(3, 1) * e(2, 3);
+  const double c3 = e(2, 1) * e(3, 2) - e(3, 1) * e(2, 2);
+  const double c2 = e(2, 0) * e(3, 3) - e(3, 0) * e(2, 3);
+  const double c1 = e(2, 0) * e(3, 2) - e(3, 0) * e(2, 2);
+  const double c0 = e(2, 0) * e(3, 1) - e(3, 0) * e(2, 1);
+  const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+  if (det == 0.0 || !std::isfinite(det)) return false;
+  double inv[4][4];  // inv[r][c]
+  inv[0][0] = (e(1, 1) * c5 - e(1, 2) * c4 + e(1, 3) * c3);
+  inv[0][1] = (-e(0, 1) * c5 + e(0, 2) * c4 - e(0, 3) * c3);
+  inv[0][2] = (e(3, 1) * s5 - e(3, 2) * s4 + e(3, 3) * s3);
+  inv[0][3] = (-e(2, 1) * s5 + e(2, 2) * s4 - e(2, 3) * s3);
+  inv[1][0] = (-e(1, 0) * c5 + e(1, 2) * c2 - e(1, 3) * c1);
+  inv[1][1] = (e(0, 0) * c5 - e(0, 2) * c2 + e(0, 3) * c1);
+  inv[1][2] = (-e(3, 0) * s5 + e(3, 2) * s2 - e(3, 3) * s1);
+  inv[1][3] = (e(2, 0) * s5 - e(2, 2) * s2 + e(2, 3) * s1);
+  inv[2][0] = (e(1, 0) * c4 - e(1, 1) * c2 + e(1, 3) * c0);
+  inv[2][1] = (-e(0, 0) * c4 + e(0, 1) * c2 - e(0, 3) * c0);
+  inv[2][2] = (e(3, 0) * s4 - e(3, 1) * s2 + e(3, 3) * s0);
+  inv[2][3] = (-e(2, 0) * s4 + e(2, 1) * s2 - e(2, 3) * s0);
+  inv[3][0] = (-e(1, 0) * c3 + e(1, 1) * c1 - e(1, 2) * c0);
+  inv[3][1] = (e(0, 0) * c3 - e(0, 1) * c1 + e(0, 2) * c0);
+  inv[3][2] = (-e(3, 0) * s3 + e(3, 1) * s1 - e(3, 2) * s0);
+  inv[3][3] = (e(2, 0) * s3 - e(2, 1) * s1 + e(2, 2) * s0);
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 4; ++r) out[c * 4 + r] = static_cast<float>(inv[r][c] / det);
+  return true;
+}
+
+bool finite3(const float* v) {
+  return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]);
+}
+
+int count_rows(int height, const sdf_tiling& t) {
+  if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0)
+    return SDF_E_INVALID_ARG;
+  const int nblocks = (height + t.block_rows - 1) / t.block_rows;
+  if (t.first_block >= nblocks) return 0;
+  // full blocks owned, then the (possibly partial) last block
+  const int owned = (nblocks - 1 - t.first_block) / t.block_stride + 1;
+  const int last = t.first_block + (owned - 1) * t.block_stride;
+  const int last_rows = height - last * t.block_rows;
+  return (owned - 1) * t.block_rows + (last_rows < t.block_rows ? last_rows : t.block_rows);
+}
+
+const sdf_tiling kWholeFrame = {8, 0, 1, 0};
+
+}  // namespace
+
+extern "C" {
+
+int sdf_abi_version(void) { return SDF_ABI_VERSION; }
+
+int sdf_defaults(sdf_scene* scene, sdf_camera* camera, sdf_light* light,
+                 sdf_material* material, sdf_params* params, int32_t width, int32_t height) {
+  if (scene) {
+    std::memset(scene, 0, sizeof(*scene));
+    scene->kind = SDF_SCENE_PRIMITIVES;
+    scene->count = 2;
+    // sceneSDF (voxel_fragment.frag:73-81): min(min(INF, planeSDF), sphereSDF)
+    sdf_primitive& plane = scene->prims[0];   // planeSDF :66-71 -> p.y
+    plane.kind = SDF_PRIM_PLANE;
+    plane.op = SDF_OP_UNION;
+    plane.p[1] = 1.0f;
+    sdf_primitive& sphere = scene->prims[1];  // sphereSDF :54-64
+    sphere.kind = SDF_PRIM_SPHERE;
+    sphere.op = SDF_OP_UNION;
+    sphere.p[1] = 0.4f;
+    sphere.p[3] = 0.2f;
+    scene->bulb_scale = 1.0f;
+    scene->bulb_iterations = 12;
+    scene->bulb_bailout = 2.0f;
+  }
+  if (camera) {
+    std::memset(camera, 0, sizeof(*camera));
+    for (int i = 0; i < 4; ++i) camera->view[i * 5] = 1.0f;  // orbit/pan 0 (main.cpp:7-11)
+    camera->eye[1] = 0.2f;                                     // :179
+    camera->eye[2] = 2.0f;
+    camera->fov_deg = 60.0f;                                   // :178
+    camera->aspect = 0.0f;                                     // AR = W / H
+    camera->pi = 3.1415925359f;                                // :15 (sic)
+  }
+  if (light) {
+    std::memset(light, 0, sizeof(*light));
+    light->pos[0] = 5.0f;                                      // :182
+    light->pos[1] = 5.0f;
+    light->ambient = 0.1f;                                     // :184
+    light->color[0] = light->color[1] = light->color[2] = 0.7f; // :183 (unused)
+  }
+  if (material) {
+    std::memset(material, 0, sizeof(*material));
+    material->amb[1] = 0.2f;                                   // :186
+    material->amb[2] = 0.8f;
+    material->dif[1] = 0.2f;                                   // :187
+    material->dif[2] = 0.8f;
+    material->ref[0] = material->ref[1] = material->ref[2] = 0.5f; // :188
+    material->shininess = 12.0f;                               // :189
+  }
+  if (params) {
+    std::memset(params, 0, sizeof(*params));
+    params->width = width > 0 ? width : 800;                   // main.cpp:4
+    params->height = height > 0 ? height : 600;                // main.cpp:5
+    params->max_steps = 100;                                   // :17
+    params->max_dist = 100.0f;                                 // :18
+    params->eps = 0.01f;                                       // :19
+    params->shadow_k = 10.0f;                                  // :205
+    params->normal_eps = 0.01f;                                // :21-23
+    params->shadow_offset = 2.0f;                              // :205
+    params->flags = SDF_FLAG_SHADOW;
+    params->normal_mode = SDF_NORMAL_CENTRAL;
+    params->ao_taps = 5;
+    params->ao_step = 0.12f;
+    params->ao_base = 0.01f;
+    params->ao_falloff = 0.95f;
+    params->ao_strength = 3.0f;
+    params->precision = SDF_PRECISION_EXACT;
+  }
+  return SDF_OK;
+}
+
+int sdf_owned_rows(int32_t height, const sdf_tiling* tiling) {
+  return count_rows(height, tiling ? *tiling : kWholeFrame);
+}
+
+int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                 const sdf_material* material, const sdf_params* params,
+                 const sdf_tiling* tiling) {
+  if (!scene || !camera || !light || !material || !params) return SDF_E_INVALID_ARG;
+  const sdf_params& p = *params;
+  if (p.width <= 0 || p.height <= 0 || p.width > 65536 || p.height > 65536)
+    return SDF_E_INVALID_ARG;
+  if (p.max_steps < 0 || p.max_steps > (1 << 24)) return SDF_E_INVALID_ARG;
+  if (!std::isfinite(p.max_dist) || !std::isfinite(p.eps) || !std::isfinite(p.shadow_k) ||
+      !std::isfinite(p.normal_eps) || !std::isfinite(p.shadow_offset))
+    return SDF_E_INVALID_ARG;
+  if (p.flags & ~(SDF_FLAG_SHADOW | SDF_FLAG_AO)) return SDF_E_INVALID_ARG;
+  if (p.normal_mode != SDF_NORMAL_CENTRAL && p.normal_mode != SDF_NORMAL_TETRA)
+    return SDF_E_INVALID_ARG;
+  if (p.precision != SDF_PRECISION_EXACT && p.precision != SDF_PRECISION_FAST)
+    return SDF_E_INVALID_ARG;
+  if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > 64)) return SDF_E_INVALID_ARG;
+  if (count_rows(p.height, tiling ? *tiling : kWholeFrame) < 0) return SDF_E_INVALID_ARG;
+  if (scene->kind == SDF_SCENE_PRIMITIVES) {
+    if (scene->count < 0 || scene->count > SDF_MAX_PRIMS) return SDF_E_INVALID_ARG;
+    for (int i = 0; i < scene->count; ++i) {
+      const sdf_primitive& pr = scene->prims[i];
+      if (pr.kind < 0 || pr.kind >= SDF_PRIM_KIND_COUNT) return SDF_E_INVALID_ARG;
+      if (pr.op < 0 || pr.op >= SDF_OP_COUNT) return SDF_E_INVALID_ARG;
+      const bool smooth = pr.op == SDF_OP_SMOOTH_UNION || pr.op == SDF_OP_SMOOTH_SUBTRACT ||
+                          pr.op == SDF_OP_SMOOTH_INTERSECT;
+      if (smooth && !(pr.k > 0.0f && std::isfinite(pr.k))) return SDF_E_INVALID_ARG;
+      for (float v : pr.p)
+        if (!std::isfinite(v)) return SDF_E_INVALID_ARG;
+    }
+  } else if (scene->kind == SDF_SCENE_MANDELBULB) {
+    if (!(scene->bulb_scale > 0.0f) || !finite3(scene->bulb_center)) return SDF_E_INVALID_ARG;
+    if (scene->bulb_iterations < 1 || scene->bulb_iterations > 64) return SDF_E_INVALID_ARG;
+    if (!(scene->bulb_bailout > 0.0f)) return SDF_E_INVALID_ARG;
+  } else {
+    return SDF_E_INVALID_ARG;
+  }
+  for (float v : camera->view)
+    if (!std::isfinite(v)) return SDF_E_INVALID_ARG;
+  if (!finite3(camera->eye) || !std::isfinite(camera->fov_deg) || !std::isfinite(camera->pi))
+    return SDF_E_INVALID_ARG;
+  if (!finite3(light->pos)) return SDF_E_INVALID_ARG;
+  float inv[16];
+  if (!invert_view(camera->view, inv)) return SDF_E_INVALID_ARG;
+  (void)material;
+  return SDF_OK;
+}
+
+int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+               const sdf_material* material, const sdf_params* params,
+               const sdf_tiling* tiling, float* rgba, int32_t* steps, void* stream) {
+  int rc = sdf_validate(scene, camera, light, material, params, tiling);
+  if (rc != SDF_OK) return rc;
+  if (!rgba) return SDF_E_INVALID_ARG;
+  const sdf_tiling t = tiling ? *tiling : kWholeFrame;
+  const int rows = count_rows(params->height, t);
+  if (rows == 0) return SDF_OK;
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SDF_E_NO_DEVICE;
+
+  sdf::KernelArgs a;
+  std::memset(&a, 0, sizeof(a));
+  invert_view(camera->view, a.inv_view);
+  const float* m = a.inv_view;
+  // :180 camera.pos = (inverse(V_mat) * vec4(camera.pos, 1)).xyz, fp32
+  for (int i = 0; i < 3; ++i)
+    a.cam[i] = m[i] * camera->eye[0] + m[4 + i] * camera->eye[1] + m[8 + i] * camera->eye[2] +
+               m[12 + i] * 1.0f;
+  // :191 -2.0f / tan(camera.fov * PI / 360.0f), fp32
+  const float ang = camera->fov_deg * camera->pi / 360.0f;
+  a.focal = -2.0f / tanf(ang);
+  a.aspect = camera->aspect > 0.0f ? camera->aspect
+                                   : (float)params->width / (float)params->height;
+  for (int i = 0; i < 3; ++i) {
+    a.light_pos[i] = light->pos[i];
+    a.mat_amb[i] = material->amb[i];
+    a.mat_dif[i] = material->dif[i];
+    a.mat_ref[i] = material->ref[i];
+  }
+  a.light_amb = light->ambient;
+  a.shininess = material->shininess;
+  a.width = params->width;
+  a.height = params->height;
+  a.max_steps = params->max_steps;
+  a.max_dist = params->max_dist;
+  a.eps = params->eps;
+  a.shadow_k = params->shadow_k;
+  a.normal_eps = params->normal_eps;
+  a.shadow_offset = params->shadow_offset;
+  a.flags = params->flags;
+  a.normal_mode = params->normal_mode;
+  a.ao_taps = (params->flags & SDF_FLAG_AO) ? params->ao_taps : 0;
+  a.ao_step = params->ao_step;
+  a.ao_base = params->ao_base;
+  a.ao_falloff = params->ao_falloff;
+  a.ao_strength = params->ao_strength;
+  a.block_rows = t.block_rows;
+  a.first_block = t.first_block;
+  a.block_stride = t.block_stride;
+  a.rows = rows;
+  a.scene_kind = scene->kind;
+  a.prim_count = scene->kind == SDF_SCENE_PRIMITIVES ? scene->count : 0;
+  for (int i = 0; i < 3; ++i) a.bulb_center[i] = scene->bulb_center[i];
+  a.bulb_scale = scene->bulb_scale;
+  a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
+  a.bulb_iterations = scene->bulb_iterations;
+  std::memcpy(a.prims, scene->prims, sizeof(a.prims));
+  a.rgba = rgba;
+  a.steps = steps;
+
+  const int variant = sdf::kVariantGeneric;
+  const int err = params->precision == SDF_PRECISION_FAST
+                      ? sdf::launch_render_fast(a, variant, stream)
+                      : sdf::launch_render_exact(a, variant, stream);
+  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+}
+
+int sdf_deinterleave(const float* parts, int32_t nparts, int32_t part_stride_rows,
+                     int32_t width, int32_t height, int32_t block_rows, float* frame,
+                     void* stream) {
+  if (!parts || !frame || nparts <= 0 || width <= 0 || height <= 0 || block_rows <= 0)
+    return SDF_E_INVALID_ARG;
+  // every part must hold its owned rows
+  for (int r = 0; r < nparts; ++r) {
+    const sdf_tiling t = {block_rows, r, nparts, 0};
+    if (count_rows(height, t) > part_stride_rows) return SDF_E_INVALID_ARG;
+  }
+  const int err = sdf::launch_deinterleave(parts, nparts, part_stride_rows, width, height,
+                                           block_rows, frame, stream);
+  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+}
+
+const char* sdf_strerror(int code) {
+  switch (code) {
+    case SDF_OK: return "success";
+    case SDF_E_INVALID_ARG: return "invalid argument";
+    case SDF_E_UNSUPPORTED: return "unsupported request";
+    case SDF_E_HIP: return "HIP runtime error";
+    case SDF_E_NO_DEVICE: return "no HIP device available";
+    default: return "unknown error";
+  }
+}
+
+}  // extern "C"

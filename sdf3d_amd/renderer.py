@@ -1,0 +1,106 @@
+"""Host-side renderer over the C-ABI (Python mirror of the C++ ``sdf::Renderer``).
+
+One ``Renderer.render`` call is one frame of the reference's draw,
+``gl->plot(sh, proj_mode)`` (/root/reference/Code/src/main.cpp:95): the scene,
+camera, light and material go in, an RGBA float framebuffer comes out.  The
+framebuffer lives in device memory allocated through PyTorch (plumbing only);
+all arithmetic runs in the HIP kernels of ``libsdf3d.so``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import abi
+from .scenes import Frame
+
+
+def tiling(rank: int = 0, world: int = 1, block_rows: int = 8) -> abi.sdf_tiling:
+    """Interleaved row-block tiling: device `rank` of `world` owns blocks
+    rank, rank + world, ...."""
+    t = abi.sdf_tiling()
+    t.block_rows, t.first_block, t.block_stride = block_rows, rank, world
+    return t
+
+
+def owned_rows(height: int, t: abi.sdf_tiling | None = None) -> int:
+    n = abi.load_library().sdf_owned_rows(height, C.byref(t) if t is not None else None)
+    if n < 0:
+        abi.check(n, "sdf_owned_rows")
+    return n
+
+
+class Renderer:
+    """Renders frames on one HIP device through ``sdf_render``."""
+
+    def __init__(self, device=None):
+        import torch
+        self.torch = torch
+        self.lib = abi.load_library()
+        if not torch.cuda.is_available():
+            raise RuntimeError("no HIP device visible: the renderer has no CPU path")
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def _stream(self, stream):
+        if stream is None:
+            stream = self.torch.cuda.current_stream(self.device)
+        return C.c_void_p(stream.cuda_stream)
+
+    def alloc(self, frame: Frame, t: abi.sdf_tiling | None = None, steps: bool = False):
+        rows = owned_rows(frame.params.height, t)
+        w = frame.params.width
+        rgba = self.torch.empty((rows, w, 4), dtype=self.torch.float32, device=self.device)
+        st = (self.torch.empty((rows, w, 2), dtype=self.torch.int32, device=self.device)
+              if steps else None)
+        return rgba, st
+
+    def render(self, frame: Frame, t: abi.sdf_tiling | None = None, out=None,
+               steps=False, stream=None):
+        """Render the rows owned by tiling `t` (None = whole frame).
+
+        Returns (rgba[rows, W, 4] float32, steps[rows, W, 2] int32 or None), both
+        on the device, asynchronous on `stream` (default: torch's current)."""
+        torch = self.torch
+        rows = owned_rows(frame.params.height, t)
+        w = frame.params.width
+        if out is None:
+            rgba, st = self.alloc(frame, t, steps is True)
+        else:
+            rgba = out
+            st = None
+        if isinstance(steps, torch.Tensor):
+            st = steps
+        if tuple(rgba.shape) != (rows, w, 4) or rgba.dtype != torch.float32 \
+                or not rgba.is_contiguous() or rgba.device != self.device:
+            raise ValueError(f"rgba must be a contiguous float32 ({rows}, {w}, 4) tensor "
+                             f"on {self.device}")
+        if st is not None and (tuple(st.shape) != (rows, w, 2) or st.dtype != torch.int32
+                               or not st.is_contiguous()):
+            raise ValueError(f"steps must be a contiguous int32 ({rows}, {w}, 2) tensor")
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdf_render(
+                C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
+                C.byref(frame.material), C.byref(frame.params),
+                C.byref(t) if t is not None else None,
+                C.c_void_p(rgba.data_ptr()),
+                C.c_void_p(st.data_ptr()) if st is not None else None,
+                self._stream(stream))
+        abi.check(rc, "sdf_render")
+        return rgba, st
+
+    def deinterleave(self, parts, nparts: int, part_stride_rows: int, width: int,
+                     height: int, block_rows: int = 8, out=None, stream=None):
+        """Scatter gathered packed row blocks (nparts x part_stride_rows rows)
+        into a full (height, width, 4) frame on this device."""
+        torch = self.torch
+        if out is None:
+            out = torch.empty((height, width, 4), dtype=torch.float32, device=self.device)
+        if parts.numel() < nparts * part_stride_rows * width * 4 or not parts.is_contiguous():
+            raise ValueError("parts buffer too small or not contiguous")
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdf_deinterleave(C.c_void_p(parts.data_ptr()), nparts,
+                                           part_stride_rows, width, height, block_rows,
+                                           C.c_void_p(out.data_ptr()), self._stream(stream))
+        abi.check(rc, "sdf_deinterleave")
+        return out

@@ -1,0 +1,212 @@
+"""GPU parity tests: the HIP kernels (through the C-ABI) against the CPU oracle.
+
+Exact precision (IEEE div/sqrt, no contraction) must satisfy the parity policy
+of tests/parity.py against the golden fixtures and fresh oracle renders; fast
+precision (hardware sqrt/rcp, FMA) is held to the same policy.  Full-size
+(BASELINE) frames are checked through size-independent properties: step-count
+sums against the oracle's full-frame statistics, determinism, tiling
+invariance, finiteness.
+"""
+import ctypes as C
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle
+from golden.make_golden import FIXTURES, frame_for
+from parity import assert_parity, report
+from sdf3d_amd import abi, renderer as R, scenes
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+RESULTS = {}
+
+
+def gpu(rd, frame, t=None, steps=True):
+    import torch
+    rgba, st = rd.render(frame, t, steps=steps)
+    torch.cuda.synchronize()
+    return rgba.cpu().numpy(), (st.cpu().numpy() if st is not None else None)
+
+
+def with_precision(frame, prec):
+    f = frame.copy()
+    f.params.precision = prec
+    return f
+
+
+def log(key, rep):
+    RESULTS[key] = rep
+    print(key, json.dumps(rep))
+
+
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+@pytest.mark.parametrize("name", sorted(FIXTURES))
+def test_fixture_parity(renderer, name, prec):
+    z = np.load(GOLD / f"{name}.npz")
+    f = with_precision(frame_for(name), prec)
+    rgba, steps = gpu(renderer, f)
+    twin, _ = oracle.render(frame_for(name), twin=True)
+    rep = report(rgba, steps, z["rgba"], z["steps"], twin)
+    log(f"fixture/{name}/{'exact' if prec == 0 else 'fast'}", rep)
+    assert_parity(rep, what=name)
+
+
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+@pytest.mark.parametrize("cfg,w,h,pose", [
+    ("REF", 800, 600, 0), ("REF", 640, 360, 2), ("C1", 512, 512, 0), ("C2", 640, 360, 3),
+    ("C3", 480, 270, 2), ("C5", 320, 180, 0)])
+def test_fresh_oracle_parity(renderer, cfg, w, h, pose, prec):
+    f = scenes.config(cfg, w, h, precision=prec, pose=pose)
+    rgba, steps = gpu(renderer, f)
+    ref_rgba, ref_steps = oracle.render(f)
+    twin, _ = oracle.render(f, twin=True)
+    rep = report(rgba, steps, ref_rgba, ref_steps, twin)
+    log(f"fresh/{cfg}_{w}x{h}_p{pose}/{'exact' if prec == 0 else 'fast'}", rep)
+    assert_parity(rep, what=cfg)
+
+
+def test_exact_mode_is_mostly_bit_exact(renderer):
+    """Exact precision executes the oracle's fp32 operation sequence; only the
+    transcendental pow (specular) may differ by an ulp."""
+    f = scenes.config("REF", 320, 180)
+    rgba, steps = gpu(renderer, f)
+    ref, ref_steps = oracle.render(f)
+    assert np.array_equal(steps, ref_steps)
+    rep = report(rgba, steps, ref, ref_steps)
+    log("bitexact/REF_320x180", rep)
+    assert rep["max_err"] < 1e-6
+
+
+@pytest.mark.parametrize("op", range(abi.OP_COUNT))
+def test_every_csg_op(renderer, op):
+    f = scenes.config("C3", 160, 90)
+    for i in range(2, f.scene.count):
+        f.scene.prims[i].op = op
+        f.scene.prims[i].k = 0.1
+    rgba, steps = gpu(renderer, f)
+    ref, ref_steps = oracle.render(f)
+    rep = report(rgba, steps, ref, ref_steps, oracle.render(f, twin=True)[0])
+    log(f"csg_op/{abi.OP_NAMES[op]}", rep)
+    assert_parity(rep, what=abi.OP_NAMES[op])
+
+
+@pytest.mark.parametrize("mutate,name", [
+    (lambda f: setattr(f.params, "normal_mode", abi.NORMAL_TETRA), "ref_tetra"),
+    (lambda f: setattr(f.params, "flags", abi.FLAG_SHADOW | abi.FLAG_AO), "ref_ao"),
+    (lambda f: setattr(f.params, "flags", 0), "ref_noshadow"),
+    (lambda f: setattr(f.params, "max_steps", 0), "max_steps_0"),
+    (lambda f: setattr(f.params, "max_steps", 1), "max_steps_1"),
+    (lambda f: setattr(f.params, "ao_taps", 1) or setattr(f.params, "flags", 3), "ao_1tap"),
+    (lambda f: setattr(f.camera, "aspect", 2.5), "explicit_AR"),
+])
+def test_feature_variants(renderer, mutate, name):
+    f = scenes.config("REF", 96, 64)
+    mutate(f)
+    rgba, steps = gpu(renderer, f)
+    ref, ref_steps = oracle.render(f)
+    rep = report(rgba, steps, ref, ref_steps, oracle.render(f, twin=True)[0])
+    log(f"variant/{name}", rep)
+    assert_parity(rep, what=name)
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (1, 9), (33, 1), (37, 23), (63, 65), (257, 9)])
+def test_ragged_sizes(renderer, w, h):
+    for prec in (abi.PRECISION_EXACT, abi.PRECISION_FAST):
+        f = scenes.config("C3", w, h, precision=prec, pose=1)
+        rgba, steps = gpu(renderer, f)
+        ref, ref_steps = oracle.render(f)
+        rep = report(rgba, steps, ref, ref_steps, oracle.render(f, twin=True)[0])
+        assert_parity(rep, what=f"{w}x{h}/{prec}")
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_tiling_and_deinterleave_reassemble_frame(renderer, world):
+    """Pixels are independent: rendering interleaved row blocks per rank and
+    scattering them back must reproduce the whole frame bit for bit."""
+    import torch
+    f = scenes.config("C3", 480, 270, precision=abi.PRECISION_FAST, pose=1)
+    whole, _ = renderer.render(f)
+    stride = R.owned_rows(f.params.height, R.tiling(0, world))
+    parts = torch.zeros((world * stride, f.params.width, 4), dtype=torch.float32,
+                        device=renderer.device)
+    for r in range(world):
+        t = R.tiling(r, world)
+        n = R.owned_rows(f.params.height, t)
+        renderer.render(f, t, out=parts[r * stride:r * stride + n])
+    frame = renderer.deinterleave(parts, world, stride, f.params.width, f.params.height)
+    torch.cuda.synchronize()
+    assert torch.equal(frame.view(torch.int32), whole.view(torch.int32))
+    # oracle agrees on one rank's packed part
+    t = R.tiling(world - 1, world)
+    n = R.owned_rows(f.params.height, t)
+    ref, _ = oracle.render(f, t)
+    part = parts[(world - 1) * stride:(world - 1) * stride + n].cpu().numpy()
+    assert_parity(report(part, None, ref, None), what="part")
+
+
+def test_empty_tiling_is_noop(renderer):
+    import torch
+    f = scenes.config("REF", 64, 16)
+    t = R.tiling(5, 8)          # owns no block of a 16-row frame
+    assert R.owned_rows(16, t) == 0
+    out = torch.empty((0, 64, 4), dtype=torch.float32, device=renderer.device)
+    renderer.render(f, t, out=out)
+    torch.cuda.synchronize()
+
+
+def test_nondefault_stream_and_determinism(renderer):
+    import torch
+    f = scenes.config("C3", 640, 360, precision=abi.PRECISION_FAST, pose=3)
+    s = torch.cuda.Stream(device=renderer.device)
+    a, _ = renderer.render(f, stream=s)
+    b, _ = renderer.render(f, stream=s)
+    s.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+@pytest.mark.parametrize("cfg", ["C4", "C2", "C5"])
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+def test_full_size_properties(renderer, cfg, prec):
+    """BASELINE-size frames: step sums match the oracle's full-frame statistics
+    (tests/golden/stats_*.npz) row by row up to branch flips; output finite,
+    alpha 1; two launches bit-identical."""
+    import torch
+    f = scenes.config(cfg, precision=prec)
+    rgba, st = renderer.render(f, steps=True)
+    rgba2, _ = renderer.render(f)
+    torch.cuda.synchronize()
+    assert torch.equal(rgba.view(torch.int32), rgba2.view(torch.int32))
+    assert bool(torch.isfinite(rgba).all()) and bool((rgba[..., 3] == 1).all())
+    z = np.load(GOLD / f"stats_{cfg}_p0.npz")
+    sp = st[..., 0].sum(dim=1, dtype=torch.int64).cpu().numpy()
+    ss = st[..., 1].sum(dim=1, dtype=torch.int64).cpu().numpy()
+    tot_sp, tot_ss = z["row_sp"].sum(), z["row_ss"].sum()
+    rel_sp = abs(sp.sum() - tot_sp) / max(tot_sp, 1)
+    rel_ss = abs(ss.sum() - tot_ss) / max(tot_ss, 1)
+    rows_equal = float(np.mean((sp == z["row_sp"]) & (ss == z["row_ss"])))
+    log(f"fullsize/{cfg}/{'exact' if prec == 0 else 'fast'}",
+        {"rel_sp": rel_sp, "rel_ss": rel_ss, "rows_equal": rows_equal})
+    assert rel_sp < 1e-3 and rel_ss < 1e-3
+
+
+def test_invalid_arguments_are_rejected_on_device(renderer):
+    import torch
+    lib = abi.load_library()
+    f = scenes.reference(64, 64)
+    f.params.max_steps = -3
+    out = torch.empty((64, 64, 4), dtype=torch.float32, device=renderer.device)
+    rc = lib.sdf_render(C.byref(f.scene), C.byref(f.camera), C.byref(f.light),
+                        C.byref(f.material), C.byref(f.params), None,
+                        C.c_void_p(out.data_ptr()), None, None)
+    assert rc == abi.SDF_E_INVALID_ARG
+    with pytest.raises(abi.SdfError):
+        renderer.render(f, out=out)
+
+
+def test_write_results():
+    out = Path("gpurun_out")
+    out.mkdir(exist_ok=True)
+    (out / "parity_results.json").write_text(json.dumps(RESULTS, indent=1, sort_keys=True))
