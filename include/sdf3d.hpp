@@ -1,0 +1,184 @@
+// sdf3d.hpp -- C++ host/scene API over the C-ABI of include/sdf_abi.h.
+//
+// Mirrors the shape of the reference host program (/root/reference/Code/src/
+// main.cpp): objects created once (main.cpp:48-56), the device program set up
+// once (:67-77), a per-frame draw in a loop (:87-98) and explicit cleanup
+// (:103-107).  Where the reference hard-codes the scene, camera, light and
+// material inside the fragment shader (voxel_fragment.frag:178-189), this API
+// takes them as values; sdf::Frame::reference() reproduces the hard-coded ones.
+//
+// Header-only; link against libsdf3d.so and amdhip64.  Errors are reported as
+// sdf::Error exceptions on this side of the boundary (the C-ABI itself never
+// throws).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sdf_abi.h"
+
+namespace sdf {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& what)
+      : std::runtime_error(what + ": " + sdf_strerror(c)), code(c) {}
+};
+
+inline void check(int rc, const char* what) {
+  if (rc != SDF_OK) throw Error(rc, what);
+}
+inline void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Scene builder: primitives combined left to right into d (d starts at +INF,
+// voxel_fragment.frag:75).
+class Scene {
+ public:
+  Scene() { std::memset(&s_, 0, sizeof(s_)); s_.kind = SDF_SCENE_PRIMITIVES; s_.bulb_scale = 1.0f;
+            s_.bulb_iterations = 12; s_.bulb_bailout = 2.0f; }
+  explicit Scene(const sdf_scene& s) : s_(s) {}
+
+  Scene& sphere(float cx, float cy, float cz, float r, int op = SDF_OP_UNION, float k = 0) {
+    return add(SDF_PRIM_SPHERE, op, k, {cx, cy, cz, r});
+  }
+  Scene& plane(float nx, float ny, float nz, float h, int op = SDF_OP_UNION, float k = 0) {
+    return add(SDF_PRIM_PLANE, op, k, {nx, ny, nz, h});
+  }
+  Scene& box(float cx, float cy, float cz, float hx, float hy, float hz, int op = SDF_OP_UNION,
+             float k = 0) {
+    return add(SDF_PRIM_BOX, op, k, {cx, cy, cz, hx, hy, hz});
+  }
+  Scene& round_box(float cx, float cy, float cz, float hx, float hy, float hz, float r,
+                   int op = SDF_OP_UNION, float k = 0) {
+    return add(SDF_PRIM_ROUND_BOX, op, k, {cx, cy, cz, hx, hy, hz, r});
+  }
+  Scene& torus(float cx, float cy, float cz, float R, float r, int op = SDF_OP_UNION,
+               float k = 0) {
+    return add(SDF_PRIM_TORUS, op, k, {cx, cy, cz, R, r});
+  }
+  Scene& capsule(float ax, float ay, float az, float bx, float by, float bz, float r,
+                 int op = SDF_OP_UNION, float k = 0) {
+    return add(SDF_PRIM_CAPSULE, op, k, {ax, ay, az, bx, by, bz, r});
+  }
+  Scene& cylinder(float cx, float cy, float cz, float r, float half_h, int op = SDF_OP_UNION,
+                  float k = 0) {
+    return add(SDF_PRIM_CYLINDER, op, k, {cx, cy, cz, r, half_h});
+  }
+  Scene& mandelbulb(float cx, float cy, float cz, float scale, int iterations = 12,
+                    float bailout = 2.0f) {
+    s_.kind = SDF_SCENE_MANDELBULB;
+    s_.count = 0;
+    s_.bulb_center[0] = cx; s_.bulb_center[1] = cy; s_.bulb_center[2] = cz;
+    s_.bulb_scale = scale; s_.bulb_iterations = iterations; s_.bulb_bailout = bailout;
+    return *this;
+  }
+  const sdf_scene& raw() const { return s_; }
+  sdf_scene& raw() { return s_; }
+
+ private:
+  Scene& add(int kind, int op, float k, std::initializer_list<float> p) {
+    if (s_.count >= SDF_MAX_PRIMS) throw Error(SDF_E_INVALID_ARG, "Scene: too many primitives");
+    sdf_primitive& pr = s_.prims[s_.count++];
+    std::memset(&pr, 0, sizeof(pr));
+    pr.kind = kind; pr.op = op; pr.k = k;
+    int i = 0;
+    for (float v : p) pr.p[i++] = v;
+    return *this;
+  }
+  sdf_scene s_;
+};
+
+// Everything one frame needs besides the output.
+struct Frame {
+  sdf_scene scene;
+  sdf_camera camera;
+  sdf_light light;
+  sdf_material material;
+  sdf_params params;
+
+  // The reference shader's hard-coded frame (voxel_fragment.frag:15-23,
+  // :54-81, :178-189, :205) at width x height (<= 0: 800 x 600, main.cpp:4-5).
+  static Frame reference(int width = 0, int height = 0) {
+    Frame f;
+    check(sdf_defaults(&f.scene, &f.camera, &f.light, &f.material, &f.params, width, height),
+          "sdf_defaults");
+    return f;
+  }
+  // Orbit the camera about the origin: V_mat = Rx(pitch) * Ry(yaw), column-major
+  // (the reference gets V_mat from Neutrino's arcball, main.cpp:93-94).
+  Frame& orbit(float yaw_deg, float pitch_deg) {
+    const double y = yaw_deg * M_PI / 180.0, p = pitch_deg * M_PI / 180.0;
+    const double cy = std::cos(y), sy = std::sin(y), cp = std::cos(p), sp = std::sin(p);
+    // rows of Rx*Ry
+    const double m[4][4] = {{cy, 0, sy, 0}, {sp * sy, cp, -sp * cy, 0},
+                            {-cp * sy, sp, cp * cy, 0}, {0, 0, 0, 1}};
+    for (int c = 0; c < 4; ++c)
+      for (int r = 0; r < 4; ++r) camera.view[c * 4 + r] = static_cast<float>(m[r][c]);
+    return *this;
+  }
+};
+
+// Owns a device framebuffer and renders frames into it on one HIP stream.
+class Renderer {
+ public:
+  Renderer(int width, int height, hipStream_t stream = nullptr)
+      : w_(width), h_(height), stream_(stream) {
+    check_hip(hipMalloc(&rgba_, size_t(w_) * h_ * 4 * sizeof(float)), "hipMalloc");
+  }
+  ~Renderer() { if (rgba_) (void)hipFree(rgba_); }
+  Renderer(const Renderer&) = delete;
+  Renderer& operator=(const Renderer&) = delete;
+
+  // One frame (the reference's gl->plot(sh, proj_mode), main.cpp:95).
+  void render(const Frame& f, const sdf_tiling* tiling = nullptr, int32_t* steps = nullptr) {
+    if (f.params.width != w_ || f.params.height != h_)
+      throw Error(SDF_E_INVALID_ARG, "Renderer: frame size differs from framebuffer");
+    check(sdf_render(&f.scene, &f.camera, &f.light, &f.material, &f.params, tiling, rgba_, steps,
+                     stream_),
+          "sdf_render");
+  }
+  // Blocking copy of the framebuffer (row 0 = bottom, GL order) to the host.
+  std::vector<float> download() const {
+    std::vector<float> out(size_t(w_) * h_ * 4);
+    check_hip(hipMemcpyAsync(out.data(), rgba_, out.size() * sizeof(float),
+                             hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
+    check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    return out;
+  }
+  float* device_rgba() const { return rgba_; }
+  int width() const { return w_; }
+  int height() const { return h_; }
+
+ private:
+  int w_, h_;
+  hipStream_t stream_;
+  float* rgba_ = nullptr;
+};
+
+// Binary PPM of an RGBA float framebuffer, clamped and quantised to 8 bits
+// (what the reference's window would show), flipped to top-down row order.
+inline void write_ppm(const std::string& path, const std::vector<float>& rgba, int w, int h) {
+  FILE* fp = std::fopen(path.c_str(), "wb");
+  if (!fp) throw std::runtime_error("cannot open " + path);
+  std::fprintf(fp, "P6\n%d %d\n255\n", w, h);
+  std::vector<unsigned char> row(size_t(w) * 3);
+  for (int y = h - 1; y >= 0; --y) {
+    for (int x = 0; x < w; ++x)
+      for (int c = 0; c < 3; ++c) {
+        float v = rgba[(size_t(y) * w + x) * 4 + c];
+        v = v < 0.f ? 0.f : (v > 1.f ? 1.f : v);
+        row[size_t(x) * 3 + c] = static_cast<unsigned char>(std::lround(v * 255.0f));
+      }
+    std::fwrite(row.data(), 1, row.size(), fp);
+  }
+  std::fclose(fp);
+}
+
+}  // namespace sdf

@@ -134,17 +134,22 @@ static inline REAL FN(mandelbulb)(FN(v3) q, int iters, REAL bail2) {
     REAL x = w.x, x2 = x * x, x4 = x2 * x2;
     REAL y = w.y, y2 = y * y, y4 = y2 * y2;
     REAL z = w.z, z2 = z * z, z4 = z2 * z2;
-    REAL k3 = x2 + z2;
-    REAL k3_2 = k3 * k3;
-    REAL k3_7 = k3_2 * k3_2 * k3_2 * k3;
-    REAL k2 = (REAL)1 / SQRT(k3_7);
+    /* iq's trig-free power-8 map, with the x/z factors taken in xz-normalised
+     * coordinates (xn, zn) = (x, z) / sqrt(k3): the same polynomial without
+     * the fp32 underflow of inversesqrt(k3^7) near the y axis. */
+    REAL k3 = FN(gmax)(x2 + z2, (REAL)1e-30f);
+    REAL r = (REAL)1 / SQRT(k3);
+    REAL s = k3 * r;
+    REAL xn = x * r, zn = z * r;
+    REAL xn2 = xn * xn, zn2 = zn * zn, xn4 = xn2 * xn2, zn4 = zn2 * zn2;
     REAL k1 = x4 + y4 + z4 - (REAL)6 * y2 * z2 - (REAL)6 * x2 * y2 + (REAL)2 * z2 * x2;
     REAL k4 = x2 - y2 + z2;
-    w.x = q.x + (REAL)64 * x * y * z * (x2 - z2) * k4 * (x4 - (REAL)6 * x2 * z2 + z4) * k1 * k2;
+    REAL yk = y * k4 * k1;
+    w.x = q.x + (REAL)64 * yk * xn * zn * (xn2 - zn2) * (xn4 - (REAL)6 * xn2 * zn2 + zn4) * s;
     w.y = q.y + (REAL)-16 * y2 * k3 * k4 * k4 + k1 * k1;
-    w.z = q.z + (REAL)-8 * y * k4 *
-                    (x4 * x4 - (REAL)28 * x4 * x2 * z2 + (REAL)70 * x4 * z4 -
-                     (REAL)28 * x2 * z2 * z4 + z4 * z4) * k1 * k2;
+    w.z = q.z + (REAL)-8 * yk *
+                    (xn4 * xn4 - (REAL)28 * xn4 * xn2 * zn2 + (REAL)70 * xn4 * zn4 -
+                     (REAL)28 * xn2 * zn2 * zn4 + zn4 * zn4) * s;
     m = FN(dot)(w, w);
     if (m > bail2) break;
   }

@@ -218,10 +218,10 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
                const sdf_tiling* tiling, float* rgba, int32_t* steps, void* stream) {
   int rc = sdf_validate(scene, camera, light, material, params, tiling);
   if (rc != SDF_OK) return rc;
-  if (!rgba) return SDF_E_INVALID_ARG;
   const sdf_tiling t = tiling ? *tiling : kWholeFrame;
   const int rows = count_rows(params->height, t);
-  if (rows == 0) return SDF_OK;
+  if (rows == 0) return SDF_OK;  // a rank that owns no block: nothing to write
+  if (!rgba) return SDF_E_INVALID_ARG;
 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SDF_E_NO_DEVICE;

@@ -2,7 +2,8 @@
 
 A pixel's error is its largest per-channel |delta| over RGBA.  A comparison
 passes when
-  * at least `min_frac` (99.99 %) of pixels are within `tol` (1e-4), and
+  * at least `min_frac` (99.99 %) of pixels are within `tol` (1e-4) -- on
+    frames under 10^4 pixels, at most one pixel may be outside -- and
   * every pixel above `tol` is a DIAGNOSED branch flip: the kernel's primary
     or shadow iteration count differs from the oracle's, or (when the fp64
     twin is supplied) the fp64 twin disagrees with the fp32 oracle there, and
@@ -29,22 +30,32 @@ def report(rgba, steps, ref_rgba, ref_steps, twin_rgba=None, tol=TOL):
     out = err > tol
     n = err.size
     flip = np.zeros_like(out)
+    step_mm = None
     if steps is not None and ref_steps is not None:
-        flip |= np.any(np.asarray(steps) != np.asarray(ref_steps), axis=-1)
+        sm = np.any(np.asarray(steps) != np.asarray(ref_steps), axis=-1)
+        step_mm = int(sm.sum())
+        flip |= sm
+    twin_dis = None
     if twin_rgba is not None:
-        flip |= np.abs(np.asarray(twin_rgba, np.float64) - ref_rgba).max(axis=-1) > tol
+        tw = np.abs(np.asarray(twin_rgba, np.float64) - ref_rgba).max(axis=-1) > tol
+        twin_dis = int(tw.sum())
+        flip |= tw
     return {
         "pixels": int(n),
         "bit_exact": int(np.sum(np.all(rgba.view(np.uint32) == ref_rgba.view(np.uint32), axis=-1))),
-        "within_tol_frac": float(1.0 - out.mean()),
+        "within_tol_frac": float(1.0 - out.mean()) if n else 1.0,
         "outliers": int(out.sum()),
         "undiagnosed": int(np.sum(out & ~flip)),
         "max_err": float(err.max()) if n else 0.0,
-        "step_mismatch": int(flip.sum()) if steps is not None else None,
+        "step_mismatch": step_mm,
+        "twin_disagree": twin_dis,
     }
 
 
 def assert_parity(rep, min_frac=MIN_FRAC, max_err=MAX_ERR, what=""):
-    assert rep["within_tol_frac"] >= min_frac, (what, rep)
+    """>= min_frac of pixels within tol; on small frames that is an outlier
+    budget of ceil((1 - min_frac) * pixels), at least one pixel."""
+    budget = max(1, int(np.ceil((1.0 - min_frac) * rep["pixels"] - 1e-9)))
+    assert rep["outliers"] <= budget, (what, rep)
     assert rep["undiagnosed"] == 0, (what, rep)
     assert rep["max_err"] <= max_err, (what, rep)

@@ -141,10 +141,11 @@ def test_tiling_and_deinterleave_reassemble_frame(renderer, world):
     assert torch.equal(frame.view(torch.int32), whole.view(torch.int32))
     # oracle agrees on one rank's packed part
     t = R.tiling(world - 1, world)
+    part, pst = gpu(renderer, f, t)
+    ref, ref_st = oracle.render(f, t)
     n = R.owned_rows(f.params.height, t)
-    ref, _ = oracle.render(f, t)
-    part = parts[(world - 1) * stride:(world - 1) * stride + n].cpu().numpy()
-    assert_parity(report(part, None, ref, None), what="part")
+    assert np.array_equal(part, parts[(world - 1) * stride:(world - 1) * stride + n].cpu().numpy())
+    assert_parity(report(part, pst, ref, ref_st, oracle.render(f, t, twin=True)[0]), what="part")
 
 
 def test_empty_tiling_is_noop(renderer):
