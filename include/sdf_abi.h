@@ -172,8 +172,15 @@ typedef struct {
   float ao_falloff;            /* per-tap weight decay                         */
   float ao_strength;           /* ao = clamp(1 - strength * occ, 0, 1)         */
   int32_t precision;           /* sdf_precision                                */
-  int32_t reserved[4];
+  int32_t dispatch;            /* sdf_dispatch (AUTO: compile-time scene
+                                  variant when one matches the scene)         */
+  int32_t reserved[3];
 } sdf_params;
+
+typedef enum {
+  SDF_DISPATCH_AUTO = 0,       /* specialised kernel if the scene matches one  */
+  SDF_DISPATCH_GENERIC = 1     /* always the generic primitive-list kernel     */
+} sdf_dispatch;
 
 /* Which rows of the frame a call renders.  Rows are grouped into blocks of
  * `block_rows` rows; block b (rows [b*block_rows, (b+1)*block_rows)) is

@@ -33,6 +33,7 @@ SCENE_PRIMITIVES, SCENE_MANDELBULB = 0, 1
 FLAG_SHADOW, FLAG_AO = 0x1, 0x2
 NORMAL_CENTRAL, NORMAL_TETRA = 0, 1
 PRECISION_EXACT, PRECISION_FAST = 0, 1
+DISPATCH_AUTO, DISPATCH_GENERIC = 0, 1
 
 
 class sdf_primitive(C.Structure):
@@ -70,7 +71,7 @@ class sdf_params(C.Structure):
                 ("flags", C.c_int32), ("normal_mode", C.c_int32), ("ao_taps", C.c_int32),
                 ("ao_step", C.c_float), ("ao_base", C.c_float), ("ao_falloff", C.c_float),
                 ("ao_strength", C.c_float), ("precision", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("dispatch", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class sdf_tiling(C.Structure):

@@ -52,9 +52,37 @@ int launch_render_fast(const KernelArgs& a, int variant, void* stream);
 int launch_deinterleave(const float* parts, int nparts, int part_stride_rows, int width,
                         int height, int block_rows, float* frame, void* stream);
 
-// Compile-time scene variants the dispatcher can pick (0 = generic list).
+// ---- compile-time scene variants ------------------------------------------
+// A variant fixes the (kind, op) sequence of the primitive list at compile
+// time; parameter values stay runtime uniforms.  The host picks the variant
+// whose signature equals the scene's (select_variant, sdf_abi.cpp); anything
+// else runs the generic kernel, which reads kinds and ops at run time.
+
+// Internal primitive kind: a PLANE whose normal is exactly (0,1,0), evaluated
+// as p.y + h -- the reference's planeSDF (voxel_fragment.frag:68) when h = 0.
+constexpr int kPrimPlaneY = 7;
+#define SDF_KO(kind, op) ((kind) * 8 + (op))
+
+// X(variant id, signature...)
+#define SDF_FIXED_VARIANTS(X)                                                        \
+  /* reference scene: min(min(INF, plane), sphere), voxel_fragment.frag:73-81 */   \
+  X(1, SDF_KO(kPrimPlaneY, SDF_OP_UNION), SDF_KO(SDF_PRIM_SPHERE, SDF_OP_UNION))    \
+  /* C1: single sphere */                                                          \
+  X(2, SDF_KO(SDF_PRIM_SPHERE, SDF_OP_UNION))                                      \
+  /* C3/C4: 8-primitive smooth-min CSG (sdf3d_amd/scenes.py set_csg8) */           \
+  X(3, SDF_KO(kPrimPlaneY, SDF_OP_UNION), SDF_KO(SDF_PRIM_SPHERE, SDF_OP_SMOOTH_UNION), \
+    SDF_KO(SDF_PRIM_BOX, SDF_OP_SMOOTH_UNION), SDF_KO(SDF_PRIM_TORUS, SDF_OP_SMOOTH_UNION), \
+    SDF_KO(SDF_PRIM_CAPSULE, SDF_OP_SMOOTH_UNION),                                 \
+    SDF_KO(SDF_PRIM_CYLINDER, SDF_OP_SMOOTH_UNION),                                \
+    SDF_KO(SDF_PRIM_ROUND_BOX, SDF_OP_SMOOTH_UNION),                               \
+    SDF_KO(SDF_PRIM_SPHERE, SDF_OP_SMOOTH_UNION))
+
 enum SceneVariant : int {
   kVariantGeneric = 0,
+  kVariantBulb = 100,
 };
+
+// Variant for a validated scene (kVariantGeneric when no fixed one matches).
+int select_variant(const sdf_scene& scene);
 
 }  // namespace sdf

@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 
 #include "../../include/sdf_abi.h"
 #include "kernel_args.h"
@@ -89,6 +90,35 @@ int count_rows(int height, const sdf_tiling& t) {
 const sdf_tiling kWholeFrame = {8, 0, 1, 0};
 
 }  // namespace
+
+namespace sdf {
+
+int select_variant(const sdf_scene& scene) {
+  if (scene.kind == SDF_SCENE_MANDELBULB) return kVariantBulb;
+  int sig[SDF_MAX_PRIMS];
+  const int n = scene.count;
+  for (int i = 0; i < n; ++i) {
+    const sdf_primitive& p = scene.prims[i];
+    int kind = p.kind;
+    if (kind == SDF_PRIM_PLANE && p.p[0] == 0.0f && p.p[1] == 1.0f && p.p[2] == 0.0f)
+      kind = kPrimPlaneY;
+    sig[i] = SDF_KO(kind, p.op);
+  }
+  auto match = [&](std::initializer_list<int> v) {
+    if ((int)v.size() != n) return false;
+    int i = 0;
+    for (int k : v)
+      if (sig[i++] != k) return false;
+    return true;
+  };
+#define SDF_MATCH(id, ...) \
+  if (match({__VA_ARGS__})) return id;
+  SDF_FIXED_VARIANTS(SDF_MATCH)
+#undef SDF_MATCH
+  return kVariantGeneric;
+}
+
+}  // namespace sdf
 
 extern "C" {
 
@@ -180,6 +210,8 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   if (p.normal_mode != SDF_NORMAL_CENTRAL && p.normal_mode != SDF_NORMAL_TETRA)
     return SDF_E_INVALID_ARG;
   if (p.precision != SDF_PRECISION_EXACT && p.precision != SDF_PRECISION_FAST)
+    return SDF_E_INVALID_ARG;
+  if (p.dispatch != SDF_DISPATCH_AUTO && p.dispatch != SDF_DISPATCH_GENERIC)
     return SDF_E_INVALID_ARG;
   if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > 64)) return SDF_E_INVALID_ARG;
   if (count_rows(p.height, tiling ? *tiling : kWholeFrame) < 0) return SDF_E_INVALID_ARG;
@@ -276,7 +308,9 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.rgba = rgba;
   a.steps = steps;
 
-  const int variant = sdf::kVariantGeneric;
+  const int variant = params->dispatch == SDF_DISPATCH_GENERIC && scene->kind == SDF_SCENE_PRIMITIVES
+                            ? sdf::kVariantGeneric
+                            : sdf::select_variant(*scene);
   const int err = params->precision == SDF_PRECISION_FAST
                       ? sdf::launch_render_fast(a, variant, stream)
                       : sdf::launch_render_exact(a, variant, stream);

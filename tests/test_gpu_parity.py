@@ -68,6 +68,22 @@ def test_fresh_oracle_parity(renderer, cfg, w, h, pose, prec):
     assert_parity(rep, what=cfg)
 
 
+@pytest.mark.parametrize("cfg,pose", [("REF", 0), ("C1", 0), ("C3", 1), ("C5", 0)])
+def test_specialised_matches_generic(renderer, cfg, pose):
+    """The compile-time scene variants compute the generic kernel's result:
+    bit-identical in exact precision, within the policy in fast precision."""
+    for prec in (abi.PRECISION_EXACT, abi.PRECISION_FAST):
+        f = scenes.config(cfg, 192, 108, precision=prec, pose=pose)
+        a, sa = gpu(renderer, f)
+        g = f.copy()
+        g.params.dispatch = abi.DISPATCH_GENERIC
+        b, sb = gpu(renderer, g)
+        if prec == abi.PRECISION_EXACT or cfg == "C5":
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(sa, sb)
+        else:
+            assert_parity(report(a, sa, b, sb), what=cfg)
+
+
 def test_exact_mode_is_mostly_bit_exact(renderer):
     """Exact precision executes the oracle's fp32 operation sequence; only the
     transcendental pow (specular) may differ by an ulp."""

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Collect rocprofv3 PMC counters for the bench's render kernel.
+
+Runs bench.py under rocprofv3 once per counter pass (one --pmc set per run, no
+tracing domains besides the counters themselves), averages each counter over
+the render-kernel dispatches, and writes profiles/pmc_<cfg>_<precision>.json:
+
+  hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+      FETCH_SIZE / WRITE_SIZE are kB; on gfx950 FETCH_SIZE reports half the
+      bytes of a wide coalesced read, so it is doubled (MI355X_MICROARCH.md
+      "HBM"); WRITE_SIZE is exact for 16-B-per-lane stores (our float4 stores).
+  valu_lane_util = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)   (when available)
+
+    python tools/pmc_traffic.py [--config C4] [--precision fast] [--out DIR]
+
+This script never touches the GPU itself: every profiled run is a child
+process started by rocprofv3.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import subprocess
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+PASSES = [
+    ["FETCH_SIZE"],
+    ["WRITE_SIZE"],
+    ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVE_CYCLES",
+     "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"],
+    ["SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
+     "SQ_WAIT_ANY"],
+    ["SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32",
+     "SQ_INSTS_VALU_ADD_F32"],
+]
+
+
+def run_pass(counters, cfg, prec, outdir, steps):
+    d = outdir / ("pmc_" + "_".join(c.lower() for c in counters)[:60])
+    cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run",
+           "--", sys.executable, str(ROOT / "bench.py"), "--config", cfg, "--precision", prec,
+           "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    files = list(d.rglob("*counter_collection*.csv"))
+    if r.returncode != 0 or not files:
+        return None, (r.stderr or "")[-800:]
+    vals = defaultdict(list)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if "render" not in row.get("Kernel_Name", ""):
+                    continue
+                vals[(row["Counter_Name"], row.get("Dispatch_Id"))].append(float(row["Counter_Value"]))
+    per = defaultdict(list)
+    for (name, _), v in vals.items():
+        per[name].append(sum(v))           # sum over dimensions (XCDs / SEs) per dispatch
+    return {k: sum(v) / len(v) for k, v in per.items()}, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--precision", default="fast")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--out", default="gpurun_out/pmc")
+    args = ap.parse_args()
+    outdir = ROOT / args.out
+    outdir.mkdir(parents=True, exist_ok=True)
+    res, errors = {}, {}
+    for counters in PASSES:
+        v, err = run_pass(counters, args.config, args.precision, outdir, args.steps)
+        if v is None:
+            errors[",".join(counters)] = err
+            print("pass failed:", counters, err[-300:] if err else "", flush=True)
+            continue
+        res.update(v)
+        print("pass ok:", counters, {k: v[k] for k in v}, flush=True)
+    sys.path.insert(0, str(ROOT))
+    from sdf3d_amd import scenes
+    f = scenes.config(args.config)
+    algo_bytes = f.params.width * f.params.height * 16
+    out = {"config": args.config, "precision": args.precision, "counters": res,
+           "algorithmic_bytes_per_launch": algo_bytes, "errors": errors,
+           "method": "rocprofv3 --pmc, one pass per counter set, mean over render dispatches; "
+                     "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)"}
+    if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
+        out["fetch_bytes_per_launch"] = 2 * res["FETCH_SIZE"] * 1024
+        out["write_bytes_per_launch"] = res["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
+    if res.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in res:
+        out["valu_lane_util"] = res["SQ_THREAD_CYCLES_VALU"] / (64 * res["SQ_ACTIVE_INST_VALU"])
+    p = outdir / f"pmc_{args.config}_{args.precision}.json"   # copy into profiles/ to commit
+    p.write_text(json.dumps(out, indent=1, sort_keys=True) + "\n")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
