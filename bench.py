@@ -39,7 +39,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mpixels/s (primary+shadow+AO) at 3840×2160, 1/2/4/8 MI355X"
-FP32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 vector (packed) peak
+FP32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 vector peak, 64 FLOP/clk/SIMD
 HBM_PEAK_GBS = 8000.0
 
 
@@ -126,6 +126,7 @@ def main():
     import torch.distributed as dist
     from sdf3d_amd import Renderer, abi, scenes
     from sdf3d_amd import renderer as R
+    from sdf3d_amd.multigpu import FrameDriver
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -138,65 +139,30 @@ def main():
     rd = Renderer(dev)
     t = R.tiling(rank, world, 8)
     rows = R.owned_rows(H, t)
-    stride = R.owned_rows(H, R.tiling(0, world, 8))   # rank 0 owns the most rows
-    stream = torch.cuda.current_stream(dev)
 
-    nbuf = 2 if world > 1 else 1
-    local = [torch.empty((stride, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
-    if world > 1 and rank == 0:
-        gathered = [torch.empty((world * stride, W, 4), dtype=torch.float32, device=dev)
-                    for _ in range(nbuf)]
-        frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-                      for _ in range(nbuf)]
-        side = torch.cuda.Stream(device=dev)
-        deint_done = [None] * nbuf
-    works = [None] * nbuf
+    def render_fn(out, stream):
+        rd.render(frame, t, out=out, stream=stream)
 
+    def deint_fn(parts, nparts, stride, w, h, b, out, stream):
+        rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
+
+    drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn, dist=dist if world > 1 else None)
     k_steps = args.steps + args.warmup
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
 
-    def step(i):
-        b = i % nbuf
-        if world > 1 and works[b] is not None:
-            works[b].wait()                   # gather i-2 has finished reading local[b]
-        ev0[i].record(stream)
-        rd.render(frame, t, out=local[b][:rows], stream=stream)
-        ev1[i].record(stream)
-        if world > 1:
-            if rank == 0:
-                if deint_done[b] is not None:
-                    stream.wait_event(deint_done[b])  # deinterleave i-2 has read gathered[b]
-                glist = [gathered[b][r * stride:(r + 1) * stride] for r in range(world)]
-                works[b] = dist.gather(local[b], gather_list=glist, dst=0, async_op=True)
-                with torch.cuda.stream(side):
-                    works[b].wait()
-                    rd.deinterleave(gathered[b], world, stride, W, H, 8, out=frames_out[b],
-                                    stream=side)
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    deint_done[b] = ev
-            else:
-                works[b] = dist.gather(local[b], gather_list=None, dst=0, async_op=True)
-
-    def drain():
-        for w in works:
-            if w is not None:
-                w.wait()
-        torch.cuda.synchronize(dev)
-
     log(f"[bench] rank {rank}/{world} {args.config} {W}x{H} rows={rows} "
         f"precision={args.precision} warmup={args.warmup} steps={args.steps}")
     for i in range(args.warmup):
-        step(i)
-    drain()
+        drv.step(i, ev0[i], ev1[i])
+    drv.drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.warmup, k_steps):
-        step(i)
-    drain()
+        drv.step(i, ev0[i], ev1[i])
+    drv.drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

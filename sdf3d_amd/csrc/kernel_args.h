@@ -36,8 +36,10 @@ struct KernelArgs {
   int32_t block_rows, first_block, block_stride, rows;
   // scene
   int32_t scene_kind, prim_count;
-  float bulb_center[3], bulb_scale, bulb_bail2;
+  float bulb_center[3], bulb_scale, bulb_inv_scale, bulb_bail2;
   int32_t bulb_iterations;
+  // prepared primitives (sdf_abi.cpp prepare_prims): kind, op, k,
+  // reserved = 1/k, p = per-kind parameter block (see render_kernel.inc)
   sdf_primitive prims[SDF_MAX_PRIMS];
   // outputs
   float* rgba;          // rows * width float4, packed rows

@@ -89,6 +89,45 @@ int count_rows(int height, const sdf_tiling& t) {
 
 const sdf_tiling kWholeFrame = {8, 0, 1, 0};
 
+// Per-frame preparation of the primitive parameter blocks the kernels read
+// (layouts in render_kernel.inc).  Every derived value is computed in fp32
+// with the operation order the oracle uses per evaluation (oracle_core.h), so
+// the exact-precision kernel stays bit-identical; 1/x values are only used by
+// the fast-precision kernel.
+void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
+  std::memcpy(out, s.prims, sizeof(s.prims));
+  for (int i = 0; i < s.count; ++i) {
+    const sdf_primitive& in = s.prims[i];
+    sdf_primitive& o = out[i];
+    o.reserved = in.k > 0.0f ? 1.0f / in.k : 0.0f;
+    const float* q = in.p;
+    float* p = o.p;
+    switch (in.kind) {
+      case SDF_PRIM_ROUND_BOX: {
+        const float r = q[6];
+        p[3] = q[3] - r;
+        p[4] = q[4] - r;
+        p[5] = q[5] - r;
+        p[6] = r;
+        break;
+      }
+      case SDF_PRIM_CAPSULE: {
+        const float bax = q[3] - q[0], bay = q[4] - q[1], baz = q[5] - q[2];
+        const float baba = bax * bax + bay * bay + baz * baz;
+        p[3] = bax;
+        p[4] = bay;
+        p[5] = baz;
+        p[6] = q[6];
+        p[7] = baba;
+        p[8] = 1.0f / baba;
+        break;
+      }
+      default:
+        break;
+    }
+  }
+}
+
 }  // namespace
 
 namespace sdf {
@@ -304,7 +343,8 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.bulb_scale = scene->bulb_scale;
   a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
   a.bulb_iterations = scene->bulb_iterations;
-  std::memcpy(a.prims, scene->prims, sizeof(a.prims));
+  prepare_prims(*scene, a.prims);
+  a.bulb_inv_scale = 1.0f / scene->bulb_scale;
   a.rgba = rgba;
   a.steps = steps;
 

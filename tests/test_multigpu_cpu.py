@@ -1,0 +1,94 @@
+"""Multi-rank path on the CPU: the FrameDriver used by bench.py, run with
+the gloo backend (world size 2 and 3) and a CPU stand-in for the render
+kernel (the oracle) and for sdf_deinterleave.  Rank 0's assembled frames
+must equal whole-frame renders bit for bit (pixels are independent)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from sdf3d_amd import renderer as R, scenes
+from sdf3d_amd.multigpu import (FrameDriver, deinterleave_index, deinterleave_torch,
+                                owned_row_ids, owned_rows_py)
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def frame_for(step):
+    return scenes.config("C3", 72, 43, pose=step % 4)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        step_box = [0]
+
+        def render_fn(out, stream):
+            f = frame_for(step_box[0])
+            rgba, _ = oracle.render(f, R.tiling(rank, world, 8), nthreads=1)
+            out.copy_(torch.from_numpy(rgba))
+
+        f0 = frame_for(0)
+        drv = FrameDriver(f0.params.width, f0.params.height, rank, world, torch.device("cpu"),
+                          render_fn, deinterleave_torch, dist=dist)
+        frames = []
+        for i in range(5):
+            step_box[0] = i
+            drv.step(i)
+            if i >= 1 and rank == 0:
+                pass
+        drv.drain()
+        if rank == 0:
+            # buffers hold the last nbuf frames
+            for i in (3, 4):
+                frames.append((i, drv.frame(i).clone().numpy()))
+            q.put(frames)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_frame_driver_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for i, got in frames:
+        want, _ = oracle.render(frame_for(i), nthreads=1)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), i
+
+
+@pytest.mark.parametrize("H", [1, 8, 43, 600, 2160])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_index_math_matches_c_abi(H, world):
+    stride = owned_rows_py(H, 0, world)
+    seen = np.zeros(H, dtype=int)
+    for r in range(world):
+        n = owned_rows_py(H, r, world)
+        assert n == R.owned_rows(H, R.tiling(r, world, 8))
+        ids = owned_row_ids(H, r, world)
+        assert len(ids) == n
+        seen[ids] += 1
+    assert (seen == 1).all()
+    idx = deinterleave_index(H, world, stride)
+    # row y of the frame comes from its owner's packed position
+    for r in range(world):
+        ids = owned_row_ids(H, r, world)
+        assert np.array_equal(idx[ids], r * stride + np.arange(len(ids)))
