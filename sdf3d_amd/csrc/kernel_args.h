@@ -41,6 +41,12 @@ struct KernelArgs {
   // prepared primitives (sdf_abi.cpp prepare_prims): kind, op, k,
   // reserved = 1/k, p = per-kind parameter block (see render_kernel.inc)
   sdf_primitive prims[SDF_MAX_PRIMS];
+  // culling bounds (fixed-scene kernels): per primitive {centre.xyz, K} with
+  // K = k + R + margin, R the radius of a sphere containing the primitive;
+  // and the same for the cluster of primitives [cluster_first, count)
+  float bound[SDF_MAX_PRIMS][4];
+  float cluster[4];
+  int32_t cluster_first;
   // outputs
   float* rgba;          // rows * width float4, packed rows
   int32_t* steps;       // rows * width int2 or null
@@ -78,6 +84,21 @@ constexpr int kPrimPlaneY = 7;
     SDF_KO(SDF_PRIM_CYLINDER, SDF_OP_SMOOTH_UNION),                                \
     SDF_KO(SDF_PRIM_ROUND_BOX, SDF_OP_SMOOTH_UNION),                               \
     SDF_KO(SDF_PRIM_SPHERE, SDF_OP_SMOOTH_UNION))
+
+// ---- exact bounding-volume culling -----------------------------------------
+// For op UNION, min(d, s) == d whenever s >= d; for SMOOTH_UNION,
+// smin(d, s, k) == d bit for bit whenever s >= d + k (h = 0).  Every SDF here
+// is exact, so s >= |p - c| - R for a sphere (c, R) containing the primitive.
+// A primitive can therefore be skipped -- without changing any output bit --
+// at points where |p - c| * (1 - kCullRel) >= d + k + R + kCullAbs; the
+// margins cover fp32 rounding of s and of the bound.  A plane is unbounded;
+// a hard-union sphere costs no more than its own bound.
+constexpr float kCullAbs = 1e-4f;
+constexpr float kCullRel = 1e-5f;
+constexpr bool cullable(int kind, int op) {
+  return kind != SDF_PRIM_PLANE && kind != kPrimPlaneY &&
+         (op == SDF_OP_SMOOTH_UNION || (op == SDF_OP_UNION && kind != SDF_PRIM_SPHERE));
+}
 
 enum SceneVariant : int {
   kVariantGeneric = 0,

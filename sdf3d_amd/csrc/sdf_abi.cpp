@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 #include <initializer_list>
 
@@ -125,6 +126,59 @@ void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
       default:
         break;
     }
+  }
+}
+
+// Bounding spheres and the cluster bound read by the fixed-scene kernels'
+// culling (kernel_args.h "exact bounding-volume culling").  Radii are computed
+// in double and rounded up.
+void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
+  std::memset(a.bound, 0, sizeof(a.bound));
+  a.cluster_first = s.count;
+  double cen[SDF_MAX_PRIMS][3], rad[SDF_MAX_PRIMS];
+  bool cull[SDF_MAX_PRIMS];
+  for (int i = 0; i < s.count; ++i) {
+    const sdf_primitive& pr = s.prims[i];
+    const float* q = pr.p;
+    double c[3] = {q[0], q[1], q[2]}, R = 0;
+    switch (pr.kind) {
+      case SDF_PRIM_SPHERE: R = q[3]; break;
+      case SDF_PRIM_BOX: R = std::sqrt(double(q[3]) * q[3] + double(q[4]) * q[4] + double(q[5]) * q[5]); break;
+      case SDF_PRIM_ROUND_BOX: R = std::sqrt(double(q[3]) * q[3] + double(q[4]) * q[4] + double(q[5]) * q[5]); break;
+      case SDF_PRIM_TORUS: R = double(q[3]) + q[4]; break;
+      case SDF_PRIM_CAPSULE: {
+        for (int j = 0; j < 3; ++j) c[j] = 0.5 * (double(q[j]) + q[3 + j]);
+        const double dx = double(q[3]) - q[0], dy = double(q[4]) - q[1], dz = double(q[5]) - q[2];
+        R = 0.5 * std::sqrt(dx * dx + dy * dy + dz * dz) + q[6];
+        break;
+      }
+      case SDF_PRIM_CYLINDER: R = std::sqrt(double(q[3]) * q[3] + double(q[4]) * q[4]); break;
+      default: R = 0; break;
+    }
+    R = std::fabs(R) * (1.0 + 1e-6) + 1e-6;
+    int kind = pr.kind;
+    if (kind == SDF_PRIM_PLANE && q[0] == 0.0f && q[1] == 1.0f && q[2] == 0.0f) kind = sdf::kPrimPlaneY;
+    cull[i] = sdf::cullable(kind, pr.op);
+    const double k = pr.op == SDF_OP_SMOOTH_UNION ? pr.k : 0.0;
+    for (int j = 0; j < 3; ++j) { cen[i][j] = c[j]; a.bound[i][j] = float(c[j]); }
+    rad[i] = R;
+    a.bound[i][3] = float((k + R + sdf::kCullAbs) * (1.0 + 1e-6));
+  }
+  int first = s.count;
+  while (first > 0 && cull[first - 1]) --first;
+  a.cluster_first = first;
+  if (first < s.count) {
+    double C[3] = {0, 0, 0};
+    for (int i = first; i < s.count; ++i)
+      for (int j = 0; j < 3; ++j) C[j] += cen[i][j] / (s.count - first);
+    double RC = 0, kmax = 0;
+    for (int i = first; i < s.count; ++i) {
+      const double dx = cen[i][0] - C[0], dy = cen[i][1] - C[1], dz = cen[i][2] - C[2];
+      RC = std::max(RC, std::sqrt(dx * dx + dy * dy + dz * dz) + rad[i]);
+      if (s.prims[i].op == SDF_OP_SMOOTH_UNION) kmax = std::max(kmax, double(s.prims[i].k));
+    }
+    for (int j = 0; j < 3; ++j) a.cluster[j] = float(C[j]);
+    a.cluster[3] = float((kmax + RC * (1.0 + 1e-6) + 1e-6 + sdf::kCullAbs) * (1.0 + 1e-6));
   }
 }
 
@@ -344,6 +398,7 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
   a.bulb_iterations = scene->bulb_iterations;
   prepare_prims(*scene, a.prims);
+  if (scene->kind == SDF_SCENE_PRIMITIVES) prepare_bounds(*scene, a);
   a.bulb_inv_scale = 1.0f / scene->bulb_scale;
   a.rgba = rgba;
   a.steps = steps;
