@@ -78,16 +78,14 @@ def rank_flops(frame, tiling, pose):
     return c.flops(len(ys) * frame.params.width, z["row_sp"][ys].sum(), z["row_ss"][ys].sum())
 
 
-def pmc_traffic(cfg, precision):
-    """HBM bytes per render launch from a committed rocprofv3 PMC summary
-    (profiles/pmc_<cfg>_<precision>.json, written by tools/pmc_traffic.py), or None."""
+def pmc_summary(cfg, precision):
+    """The committed rocprofv3 PMC summary of the render kernel
+    (profiles/pmc_<cfg>_<precision>.json, written by tools/pmc_traffic.py), or {}."""
     p = ROOT / "profiles" / f"pmc_{cfg}_{precision}.json"
-    if not p.exists():
-        return None
     try:
-        return float(json.loads(p.read_text())["hbm_bytes_per_launch"])
+        return json.loads(p.read_text())
     except Exception:
-        return None
+        return {}
 
 
 def cpu_baseline(frame, stride, frames):
@@ -195,12 +193,19 @@ def main():
         }
         if flops is not None:
             ach = flops / (kavg_ms * 1e-3) / 1e12
-            traffic = pmc_traffic(args.config, args.precision) if world == 1 else None
+            pmc = pmc_summary(args.config, args.precision) if world == 1 else {}
             out["roofline"] = {"bound": "valu", "achieved": round(ach, 2),
                                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(ach / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                               "frac": round(ach / FP32_PEAK_TFLOPS, 4),
+                               "traffic": pmc.get("hbm_bytes_per_launch"),
                                "flops_per_launch": flops,
                                "store_GBps": round(rows * W * 16 / (kavg_ms * 1e-3) / 1e9, 1)}
+            ex = pmc.get("executed_flops_per_launch")
+            if ex:
+                # culled primitives are algorithmic work the kernel provably
+                # need not execute; the hardware counter shows what it did run
+                out["roofline"]["executed_flops_per_launch"] = ex
+                out["roofline"]["executed_TFLOPs"] = round(ex / (kavg_ms * 1e-3) / 1e12, 2)
         else:
             out["roofline"] = None
         if world == 1 and not args.no_cpu_baseline:

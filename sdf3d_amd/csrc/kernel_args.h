@@ -95,6 +95,7 @@ constexpr int kPrimPlaneY = 7;
 // a hard-union sphere costs no more than its own bound.
 constexpr float kCullAbs = 1e-4f;
 constexpr float kCullRel = 1e-5f;
+constexpr float kCullScale = 1.0f / (1.0f - kCullRel);
 constexpr bool cullable(int kind, int op) {
   return kind != SDF_PRIM_PLANE && kind != kPrimPlaneY &&
          (op == SDF_OP_SMOOTH_UNION || (op == SDF_OP_UNION && kind != SDF_PRIM_SPHERE));

@@ -101,6 +101,7 @@ void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
     const sdf_primitive& in = s.prims[i];
     sdf_primitive& o = out[i];
     o.reserved = in.k > 0.0f ? 1.0f / in.k : 0.0f;
+    o.p[11] = in.k * 0.25f;  // smooth-min k/4 (fast precision)
     const float* q = in.p;
     float* p = o.p;
     switch (in.kind) {
@@ -162,7 +163,8 @@ void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
     const double k = pr.op == SDF_OP_SMOOTH_UNION ? pr.k : 0.0;
     for (int j = 0; j < 3; ++j) { cen[i][j] = c[j]; a.bound[i][j] = float(c[j]); }
     rad[i] = R;
-    a.bound[i][3] = float((k + R + sdf::kCullAbs) * (1.0 + 1e-6));
+    // K' = (k + R + margin) / (1 - kCullRel), rounded up (render_kernel.inc wave_near)
+    a.bound[i][3] = float((k + R + sdf::kCullAbs) / (1.0 - sdf::kCullRel) * (1.0 + 1e-6));
   }
   int first = s.count;
   while (first > 0 && cull[first - 1]) --first;
@@ -178,7 +180,8 @@ void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
       if (s.prims[i].op == SDF_OP_SMOOTH_UNION) kmax = std::max(kmax, double(s.prims[i].k));
     }
     for (int j = 0; j < 3; ++j) a.cluster[j] = float(C[j]);
-    a.cluster[3] = float((kmax + RC * (1.0 + 1e-6) + 1e-6 + sdf::kCullAbs) * (1.0 + 1e-6));
+    a.cluster[3] = float((kmax + RC * (1.0 + 1e-6) + 1e-6 + sdf::kCullAbs) /
+                         (1.0 - sdf::kCullRel) * (1.0 + 1e-6));
   }
 }
 

@@ -36,8 +36,8 @@ PASSES = [
      "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"],
     ["SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
      "SQ_WAIT_ANY"],
-    ["SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32",
-     "SQ_INSTS_VALU_ADD_F32"],
+    ["SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS", "SQ_INSTS_VALU_TRANS_F32",
+     "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32"],
 ]
 
 
@@ -93,6 +93,15 @@ def main():
         out["fetch_bytes_per_launch"] = 2 * res["FETCH_SIZE"] * 1024
         out["write_bytes_per_launch"] = res["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
+    if all(k in res for k in ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                              "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32")):
+        # hardware-counted fp32 work the (culled) kernel executed, Omniperf's VALU
+        # FLOPs formula: 64 lanes x (ADD + MUL + TRANS + 2 FMA) wave-instructions.
+        # min/max/compare are not counted by these counters (the algorithmic
+        # count does count them), so this is a lower bound on executed flops.
+        out["executed_flops_per_launch"] = 64.0 * (
+            res["SQ_INSTS_VALU_ADD_F32"] + res["SQ_INSTS_VALU_MUL_F32"]
+            + res["SQ_INSTS_VALU_TRANS_F32"] + 2.0 * res["SQ_INSTS_VALU_FMA_F32"])
     if res.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in res:
         out["valu_lane_util"] = res["SQ_THREAD_CYCLES_VALU"] / (64 * res["SQ_ACTIVE_INST_VALU"])
     p = outdir / f"pmc_{args.config}_{args.precision}.json"   # copy into profiles/ to commit
