@@ -127,7 +127,8 @@ CONFIGS = {
     "C1": (512, 512, "single sphere, 64 max steps, primary + shadow + shading (CPU plumbing)"),
     "C2": (1920, 1080, "sphere + ground plane, 128 steps, primary rays only"),
     "C3": (1920, 1080, "8-primitive smooth-min CSG + soft shadow + 5-tap AO + tetra normals"),
-    "C4": (3840, 2160, "C3 scene at 3840x2160"),
+    "C4": (3840, 2160, "8-primitive smooth-min CSG + soft shadow + 5-tap AO + tetra normals, "
+                       "3840x2160"),
     "C5": (3840, 2160, "Mandelbulb power 8, 12-iteration DE, shadow + AO + tetra normals"),
     "REF": (800, 600, "the reference shader exactly (plane + sphere, 100 steps, shadow)"),
 }
