@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--precision", default="fast", choices=["fast", "exact"])
     ap.add_argument("--pose", type=int, default=0)
+    ap.add_argument("--format", default="rgba32f", choices=["rgba32f", "rgba16f", "rgba8"],
+                    help="framebuffer format written by the kernel and gathered (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-stride", type=int, default=4,
                     help="CPU baseline renders every k-th 8-row block of the frame")
@@ -86,6 +88,11 @@ def pmc_summary(cfg, precision):
         return json.loads(p.read_text())
     except Exception:
         return {}
+
+
+def lib_bpp(frame):
+    from sdf3d_amd import abi
+    return abi.load_library().sdf_format_bytes(frame.params.output_format)
 
 
 def cpu_baseline(frame, stride, frames):
@@ -133,6 +140,7 @@ def main():
 
     prec = abi.PRECISION_FAST if args.precision == "fast" else abi.PRECISION_EXACT
     frame = scenes.config(args.config, precision=prec, pose=args.pose)
+    frame.params.output_format = abi.FORMAT_NAMES[args.format]
     W, H = frame.params.width, frame.params.height
     rd = Renderer(dev)
     t = R.tiling(rank, world, 8)
@@ -144,7 +152,9 @@ def main():
     def deint_fn(parts, nparts, stride, w, h, b, out, stream):
         rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
 
-    drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn, dist=dist if world > 1 else None)
+    drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
+                      dist=dist if world > 1 else None,
+                      dtype=R.torch_dtype(frame.params.output_format))
     k_steps = args.steps + args.warmup
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
@@ -185,6 +195,7 @@ def main():
             "config": {"workload": f"{args.config}: {frame.meta['description']}",
                        "width": W, "height": H, "max_steps": frame.params.max_steps,
                        "precision": args.precision, "pose": args.pose,
+                       "format": args.format,
                        "tiling": "8-row interleaved blocks" if world > 1 else "whole frame",
                        "gather": "RCCL gather to rank 0 + sdf_deinterleave" if world > 1
                        else None},
@@ -193,13 +204,15 @@ def main():
         }
         if flops is not None:
             ach = flops / (kavg_ms * 1e-3) / 1e12
-            pmc = pmc_summary(args.config, args.precision) if world == 1 else {}
+            pmc = (pmc_summary(args.config, args.precision)
+                   if world == 1 and args.format == "rgba32f" else {})
             out["roofline"] = {"bound": "valu", "achieved": round(ach, 2),
                                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(ach / FP32_PEAK_TFLOPS, 4),
                                "traffic": pmc.get("hbm_bytes_per_launch"),
                                "flops_per_launch": flops,
-                               "store_GBps": round(rows * W * 16 / (kavg_ms * 1e-3) / 1e9, 1)}
+                               "store_GBps": round(rows * W * lib_bpp(frame) / (kavg_ms * 1e-3)
+                                                   / 1e9, 1)}
             ex = pmc.get("executed_flops_per_launch")
             if ex:
                 # culled primitives are algorithmic work the kernel provably

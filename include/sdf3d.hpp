@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <stdexcept>
 #include <string>
@@ -126,11 +127,12 @@ struct Frame {
 };
 
 // Owns a device framebuffer and renders frames into it on one HIP stream.
+// The buffer holds width x height pixels of up to 16 bytes (any sdf_format).
 class Renderer {
  public:
   Renderer(int width, int height, hipStream_t stream = nullptr)
       : w_(width), h_(height), stream_(stream) {
-    check_hip(hipMalloc(&rgba_, size_t(w_) * h_ * 4 * sizeof(float)), "hipMalloc");
+    check_hip(hipMalloc(&rgba_, size_t(w_) * h_ * 16), "hipMalloc");
   }
   ~Renderer() { if (rgba_) (void)hipFree(rgba_); }
   Renderer(const Renderer&) = delete;
@@ -144,12 +146,18 @@ class Renderer {
                      stream_),
           "sdf_render");
   }
-  // Blocking copy of the framebuffer (row 0 = bottom, GL order) to the host.
+  // Blocking copy of an RGBA32F framebuffer (row 0 = bottom, GL order).
   std::vector<float> download() const {
     std::vector<float> out(size_t(w_) * h_ * 4);
-    check_hip(hipMemcpyAsync(out.data(), rgba_, out.size() * sizeof(float),
-                             hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
-    check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    copy_out(out.data(), out.size() * sizeof(float));
+    return out;
+  }
+  // Blocking copy of the framebuffer bytes of any format.
+  std::vector<unsigned char> download_bytes(int format) const {
+    const int bpp = sdf_format_bytes(format);
+    if (bpp < 0) throw Error(bpp, "download_bytes");
+    std::vector<unsigned char> out(size_t(w_) * h_ * bpp);
+    copy_out(out.data(), out.size());
     return out;
   }
   float* device_rgba() const { return rgba_; }
@@ -157,6 +165,11 @@ class Renderer {
   int height() const { return h_; }
 
  private:
+  void copy_out(void* dst, size_t bytes) const {
+    check_hip(hipMemcpyAsync(dst, rgba_, bytes, hipMemcpyDeviceToHost, stream_),
+              "hipMemcpyAsync");
+    check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+  }
   int w_, h_;
   hipStream_t stream_;
   float* rgba_ = nullptr;

@@ -174,8 +174,21 @@ typedef struct {
   int32_t precision;           /* sdf_precision                                */
   int32_t dispatch;            /* sdf_dispatch (AUTO: compile-time scene
                                   variant when one matches the scene)         */
-  int32_t reserved[3];
+  int32_t output_format;       /* sdf_format of the framebuffer written       */
+  int32_t reserved[2];
 } sdf_params;
+
+/* Framebuffer element formats (4 channels R,G,B,A per pixel).
+ *   RGBA32F  the shader's float fragment_color (voxel_fragment.frag:12,210).
+ *   RGBA16F  IEEE half, round to nearest even.
+ *   RGBA8    what the reference's RGBA8 window shows (main.cpp:95-96):
+ *            u8 = trunc(min(max(c, 0), 1) * 255 + 0.5), NaN -> 0, no
+ *            multiply-add fusion.                                          */
+typedef enum {
+  SDF_FORMAT_RGBA32F = 0,
+  SDF_FORMAT_RGBA16F = 1,
+  SDF_FORMAT_RGBA8 = 2
+} sdf_format;
 
 typedef enum {
   SDF_DISPATCH_AUTO = 0,       /* specialised kernel if the scene matches one  */
@@ -215,23 +228,28 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera,
  * negative SDF_E* code. */
 int sdf_owned_rows(int32_t height, const sdf_tiling* tiling);
 
+/* Bytes per pixel of a sdf_format (16, 8, 4), or a negative SDF_E* code. */
+int sdf_format_bytes(int32_t format);
+
 /* Render the rows owned by `tiling` (NULL = whole frame) into `rgba`
- * (device, owned_rows * width * 4 floats, packed as described above).
+ * (device, owned_rows * width pixels of params->output_format, packed as
+ * described above).
  * `steps` (device, may be NULL) receives 2 int32 per pixel: the primary and
  * the shadow march iteration counts (diagnostics / flop accounting).
  * Asynchronous on `stream`. */
 int sdf_render(const sdf_scene* scene, const sdf_camera* camera,
                const sdf_light* light, const sdf_material* material,
                const sdf_params* params, const sdf_tiling* tiling,
-               float* rgba, int32_t* steps, void* stream);
+               void* rgba, int32_t* steps, void* stream);
 
 /* Scatter `nparts` packed row-block buffers (part r = rank r's output for
  * tiling {block_rows, r, nparts}), laid out back to back in `parts` with a
  * pitch of `part_stride_rows` rows each, into the full frame `frame`
- * (height * width * 4 floats).  Device pointers; asynchronous on `stream`. */
-int sdf_deinterleave(const float* parts, int32_t nparts,
+ * (height * width pixels of `format`).  Device pointers; asynchronous on
+ * `stream`. */
+int sdf_deinterleave(const void* parts, int32_t nparts,
                      int32_t part_stride_rows, int32_t width, int32_t height,
-                     int32_t block_rows, float* frame, void* stream);
+                     int32_t block_rows, int32_t format, void* frame, void* stream);
 
 /* Short description of a status code. */
 const char* sdf_strerror(int code);

@@ -34,6 +34,8 @@ FLAG_SHADOW, FLAG_AO = 0x1, 0x2
 NORMAL_CENTRAL, NORMAL_TETRA = 0, 1
 PRECISION_EXACT, PRECISION_FAST = 0, 1
 DISPATCH_AUTO, DISPATCH_GENERIC = 0, 1
+FORMAT_RGBA32F, FORMAT_RGBA16F, FORMAT_RGBA8 = 0, 1, 2
+FORMAT_NAMES = {"rgba32f": FORMAT_RGBA32F, "rgba16f": FORMAT_RGBA16F, "rgba8": FORMAT_RGBA8}
 
 
 class sdf_primitive(C.Structure):
@@ -71,7 +73,8 @@ class sdf_params(C.Structure):
                 ("flags", C.c_int32), ("normal_mode", C.c_int32), ("ao_taps", C.c_int32),
                 ("ao_step", C.c_float), ("ao_base", C.c_float), ("ao_falloff", C.c_float),
                 ("ao_strength", C.c_float), ("precision", C.c_int32),
-                ("dispatch", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("dispatch", C.c_int32), ("output_format", C.c_int32),
+                ("reserved", C.c_int32 * 2)]
 
 
 class sdf_tiling(C.Structure):
@@ -96,7 +99,8 @@ SIGNATURES = {
     "sdf_render": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light), _P(sdf_material),
                              _P(sdf_params), _P(sdf_tiling), C.c_void_p, C.c_void_p, C.c_void_p]),
     "sdf_deinterleave": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
-                                   C.c_int32, C.c_void_p, C.c_void_p]),
+                                   C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "sdf_format_bytes": (C.c_int, [C.c_int32]),
     "sdf_strerror": (C.c_char_p, [C.c_int]),
 }
 

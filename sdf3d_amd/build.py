@@ -75,6 +75,21 @@ def build_library(force: bool = False, verbose: bool = True) -> Path:
     return LIB
 
 
+BIN_DIR = PKG / "bin"
+EXAMPLE = ROOT / "examples" / "sdf_main.cpp"
+
+
+def build_example(force: bool = False, verbose: bool = True) -> Path:
+    """The headless C++ host program over include/sdf3d.hpp (links libsdf3d.so)."""
+    BIN_DIR.mkdir(parents=True, exist_ok=True)
+    exe = BIN_DIR / "sdf_main"
+    deps = [EXAMPLE, ROOT / "include" / "sdf3d.hpp", ROOT / "include" / "sdf_abi.h", LIB]
+    if force or _stale(exe, deps):
+        _run([_hipcc(), "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-I", ROOT / "include",
+              EXAMPLE, "-L", LIB_DIR, "-lsdf3d", "-Wl,-rpath,$ORIGIN/../lib", "-o", exe], verbose)
+    return exe
+
+
 def build_oracle(verbose: bool = True) -> Path:
     """Compile the CPU oracle (test infrastructure) with its own Makefile."""
     _run(["make", "-s", "-C", ROOT / "oracle"], verbose)
@@ -83,4 +98,5 @@ def build_oracle(verbose: bool = True) -> Path:
 
 if __name__ == "__main__":
     build_library(force="--force" in sys.argv)
+    build_example(force="--force" in sys.argv)
     build_oracle()

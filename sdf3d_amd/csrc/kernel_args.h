@@ -29,7 +29,7 @@ struct KernelArgs {
   int32_t width, height;
   int32_t max_steps;
   float max_dist, eps, shadow_k, normal_eps, shadow_offset;
-  int32_t flags, normal_mode;
+  int32_t flags, normal_mode, format;
   int32_t ao_taps;
   float ao_step, ao_base, ao_falloff, ao_strength;
   // tiling
@@ -48,7 +48,7 @@ struct KernelArgs {
   float cluster[4];
   int32_t cluster_first;
   // outputs
-  float* rgba;          // rows * width float4, packed rows
+  void* rgba;           // rows * width pixels of `format`, packed rows
   int32_t* steps;       // rows * width int2 or null
 };
 
@@ -57,8 +57,8 @@ struct KernelArgs {
 // (see render_kernel.inc).  Return a hipError_t as int.
 int launch_render_exact(const KernelArgs& a, int variant, void* stream);
 int launch_render_fast(const KernelArgs& a, int variant, void* stream);
-int launch_deinterleave(const float* parts, int nparts, int part_stride_rows, int width,
-                        int height, int block_rows, float* frame, void* stream);
+int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int row_bytes,
+                        int height, int block_rows, void* frame, void* stream);
 
 // ---- compile-time scene variants ------------------------------------------
 // A variant fixes the (kind, op) sequence of the primitive list at compile

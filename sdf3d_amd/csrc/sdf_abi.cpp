@@ -309,6 +309,7 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
     return SDF_E_INVALID_ARG;
   if (p.dispatch != SDF_DISPATCH_AUTO && p.dispatch != SDF_DISPATCH_GENERIC)
     return SDF_E_INVALID_ARG;
+  if (sdf_format_bytes(p.output_format) < 0) return SDF_E_INVALID_ARG;
   if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > 64)) return SDF_E_INVALID_ARG;
   if (count_rows(p.height, tiling ? *tiling : kWholeFrame) < 0) return SDF_E_INVALID_ARG;
   if (scene->kind == SDF_SCENE_PRIMITIVES) {
@@ -341,9 +342,18 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   return SDF_OK;
 }
 
+int sdf_format_bytes(int32_t format) {
+  switch (format) {
+    case SDF_FORMAT_RGBA32F: return 16;
+    case SDF_FORMAT_RGBA16F: return 8;
+    case SDF_FORMAT_RGBA8: return 4;
+    default: return SDF_E_INVALID_ARG;
+  }
+}
+
 int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
                const sdf_material* material, const sdf_params* params,
-               const sdf_tiling* tiling, float* rgba, int32_t* steps, void* stream) {
+               const sdf_tiling* tiling, void* rgba, int32_t* steps, void* stream) {
   int rc = sdf_validate(scene, camera, light, material, params, tiling);
   if (rc != SDF_OK) return rc;
   const sdf_tiling t = tiling ? *tiling : kWholeFrame;
@@ -385,6 +395,7 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.shadow_offset = params->shadow_offset;
   a.flags = params->flags;
   a.normal_mode = params->normal_mode;
+  a.format = params->output_format;
   a.ao_taps = (params->flags & SDF_FLAG_AO) ? params->ao_taps : 0;
   a.ao_step = params->ao_step;
   a.ao_base = params->ao_base;
@@ -415,17 +426,19 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 
-int sdf_deinterleave(const float* parts, int32_t nparts, int32_t part_stride_rows,
-                     int32_t width, int32_t height, int32_t block_rows, float* frame,
-                     void* stream) {
-  if (!parts || !frame || nparts <= 0 || width <= 0 || height <= 0 || block_rows <= 0)
+int sdf_deinterleave(const void* parts, int32_t nparts, int32_t part_stride_rows,
+                     int32_t width, int32_t height, int32_t block_rows, int32_t format,
+                     void* frame, void* stream) {
+  const int bpp = sdf_format_bytes(format);
+  if (bpp < 0 || !parts || !frame || nparts <= 0 || width <= 0 || height <= 0 ||
+      block_rows <= 0)
     return SDF_E_INVALID_ARG;
   // every part must hold its owned rows
   for (int r = 0; r < nparts; ++r) {
     const sdf_tiling t = {block_rows, r, nparts, 0};
     if (count_rows(height, t) > part_stride_rows) return SDF_E_INVALID_ARG;
   }
-  const int err = sdf::launch_deinterleave(parts, nparts, part_stride_rows, width, height,
+  const int err = sdf::launch_deinterleave(parts, nparts, part_stride_rows, width * bpp, height,
                                            block_rows, frame, stream);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }

@@ -53,7 +53,7 @@ def deinterleave_index(height: int, world: int, stride: int, block_rows: int = 8
 class FrameDriver:
     def __init__(self, width: int, height: int, rank: int, world: int, device,
                  render_fn: Callable, deinterleave_fn: Callable, block_rows: int = 8,
-                 nbuf: int = 2, dist=None):
+                 nbuf: int = 2, dist=None, dtype=None):
         import torch
         self.torch = torch
         self.W, self.H = width, height
@@ -67,7 +67,8 @@ class FrameDriver:
         self.stride = owned_rows_py(height, 0, world, block_rows)  # rank 0 owns the most
         self.gpu = getattr(device, "type", str(device)).startswith("cuda")
         self.nbuf = nbuf if world > 1 else 1
-        mk = lambda *shape: torch.empty(shape, dtype=torch.float32, device=device)  # noqa: E731
+        dtype = dtype or torch.float32   # the framebuffer format on the wire
+        mk = lambda *shape: torch.empty(shape, dtype=dtype, device=device)  # noqa: E731
         self.local = [mk(self.stride, width, 4) for _ in range(self.nbuf)]
         self.works = [None] * self.nbuf
         self.root = rank == 0

@@ -29,6 +29,13 @@ def owned_rows(height: int, t: abi.sdf_tiling | None = None) -> int:
     return n
 
 
+def torch_dtype(fmt: int):
+    """torch element type of a framebuffer format (4 channels per pixel)."""
+    import torch
+    return {abi.FORMAT_RGBA32F: torch.float32, abi.FORMAT_RGBA16F: torch.float16,
+            abi.FORMAT_RGBA8: torch.uint8}[fmt]
+
+
 class Renderer:
     """Renders frames on one HIP device through ``sdf_render``."""
 
@@ -50,7 +57,8 @@ class Renderer:
     def alloc(self, frame: Frame, t: abi.sdf_tiling | None = None, steps: bool = False):
         rows = owned_rows(frame.params.height, t)
         w = frame.params.width
-        rgba = self.torch.empty((rows, w, 4), dtype=self.torch.float32, device=self.device)
+        rgba = self.torch.empty((rows, w, 4), dtype=torch_dtype(frame.params.output_format),
+                                device=self.device)
         st = (self.torch.empty((rows, w, 2), dtype=self.torch.int32, device=self.device)
               if steps else None)
         return rgba, st
@@ -71,9 +79,10 @@ class Renderer:
             st = None
         if isinstance(steps, torch.Tensor):
             st = steps
-        if tuple(rgba.shape) != (rows, w, 4) or rgba.dtype != torch.float32 \
+        dt = torch_dtype(frame.params.output_format)
+        if tuple(rgba.shape) != (rows, w, 4) or rgba.dtype != dt \
                 or not rgba.is_contiguous() or rgba.device != self.device:
-            raise ValueError(f"rgba must be a contiguous float32 ({rows}, {w}, 4) tensor "
+            raise ValueError(f"rgba must be a contiguous {dt} ({rows}, {w}, 4) tensor "
                              f"on {self.device}")
         if st is not None and (tuple(st.shape) != (rows, w, 2) or st.dtype != torch.int32
                                or not st.is_contiguous()):
@@ -90,17 +99,22 @@ class Renderer:
         return rgba, st
 
     def deinterleave(self, parts, nparts: int, part_stride_rows: int, width: int,
-                     height: int, block_rows: int = 8, out=None, stream=None):
+                     height: int, block_rows: int = 8, out=None, stream=None,
+                     fmt: int | None = None):
         """Scatter gathered packed row blocks (nparts x part_stride_rows rows)
         into a full (height, width, 4) frame on this device."""
         torch = self.torch
+        if fmt is None:
+            fmt = {torch.float32: abi.FORMAT_RGBA32F, torch.float16: abi.FORMAT_RGBA16F,
+                   torch.uint8: abi.FORMAT_RGBA8}[parts.dtype]
         if out is None:
-            out = torch.empty((height, width, 4), dtype=torch.float32, device=self.device)
-        if parts.numel() < nparts * part_stride_rows * width * 4 or not parts.is_contiguous():
-            raise ValueError("parts buffer too small or not contiguous")
+            out = torch.empty((height, width, 4), dtype=torch_dtype(fmt), device=self.device)
+        if parts.numel() < nparts * part_stride_rows * width * 4 or not parts.is_contiguous() \
+                or parts.dtype != torch_dtype(fmt) or out.dtype != parts.dtype:
+            raise ValueError("parts buffer too small, not contiguous or of another format")
         with torch.cuda.device(self.device):
             rc = self.lib.sdf_deinterleave(C.c_void_p(parts.data_ptr()), nparts,
-                                           part_stride_rows, width, height, block_rows,
+                                           part_stride_rows, width, height, block_rows, fmt,
                                            C.c_void_p(out.data_ptr()), self._stream(stream))
         abi.check(rc, "sdf_deinterleave")
         return out

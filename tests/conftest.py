@@ -26,6 +26,11 @@ def pytest_configure(config):
 def renderer():
     import torch
     from sdf3d_amd import Renderer
+    from sdf3d_amd import build as b
+    # a fresh checkout builds the in-tree library and host program first (no-op
+    # when they are up to date)
+    b.build_library(verbose=False)
+    b.build_example(verbose=False)
     # GPU tests must not pass silently without a device: fail, do not skip.
     assert torch.cuda.is_available(), "gpu test run without a visible HIP device"
     return Renderer("cuda:0")

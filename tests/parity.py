@@ -19,6 +19,20 @@ MIN_FRAC = 0.9999
 MAX_ERR = 0.05
 
 
+def quantize(rgba, fmt):
+    """Reference conversion of float RGBA to a framebuffer format (sdf_abi.h
+    sdf_format): 0 rgba32f, 1 rgba16f (round to nearest even), 2 rgba8
+    (trunc(min(max(c,0),1) * 255 + 0.5), NaN -> 0, fp32 mul then add)."""
+    a = np.asarray(rgba, dtype=np.float32)
+    if fmt == 0:
+        return a
+    if fmt == 1:
+        return a.astype(np.float16)
+    q = np.fmin(np.fmax(a, np.float32(0)), np.float32(1))   # fmax/fmin drop NaN -> 0
+    q = np.nan_to_num(q, nan=0.0).astype(np.float32)
+    return ((q * np.float32(255)).astype(np.float32) + np.float32(0.5)).astype(np.uint8)
+
+
 def report(rgba, steps, ref_rgba, ref_steps, twin_rgba=None, tol=TOL):
     rgba = np.asarray(rgba, dtype=np.float32)
     ref_rgba = np.asarray(ref_rgba, dtype=np.float32)

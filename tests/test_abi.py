@@ -81,6 +81,8 @@ def test_validate_accepts_all_configs():
     lambda f: setattr(f.params, "flags", 0x80),
     lambda f: setattr(f.params, "normal_mode", 7),
     lambda f: setattr(f.params, "precision", 9),
+    lambda f: setattr(f.params, "output_format", 7),
+    lambda f: setattr(f.params, "dispatch", 3),
     lambda f: setattr(f.params, "eps", float("nan")),
     lambda f: setattr(f.scene, "count", abi.SDF_MAX_PRIMS + 1),
     lambda f: setattr(f.scene.prims[0], "kind", 99),
@@ -110,7 +112,8 @@ def test_render_rejects_null_output():
     rc = lib.sdf_render(C.byref(f.scene), C.byref(f.camera), C.byref(f.light),
                         C.byref(f.material), C.byref(f.params), None, None, None, None)
     assert rc == abi.SDF_E_INVALID_ARG
-    assert lib.sdf_deinterleave(None, 1, 1, 1, 1, 8, None, None) == abi.SDF_E_INVALID_ARG
+    assert lib.sdf_deinterleave(None, 1, 1, 1, 1, 8, 0, None, None) == abi.SDF_E_INVALID_ARG
+    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3)] == [16, 8, 4, abi.SDF_E_INVALID_ARG]
 
 
 @pytest.mark.parametrize("height", [1, 7, 8, 9, 23, 600, 1080, 2160])

@@ -16,7 +16,7 @@ import pytest
 
 import oracle
 from golden.make_golden import FIXTURES, frame_for
-from parity import BULB_FAST, assert_parity, report
+from parity import BULB_FAST, assert_parity, quantize, report
 from sdf3d_amd import abi, renderer as R, scenes
 
 pytestmark = pytest.mark.gpu
@@ -225,7 +225,69 @@ def test_invalid_arguments_are_rejected_on_device(renderer):
         renderer.render(f, out=out)
 
 
+@pytest.mark.parametrize("fmt", [abi.FORMAT_RGBA16F, abi.FORMAT_RGBA8])
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+def test_output_formats(renderer, fmt, prec):
+    """RGBA16F / RGBA8 framebuffers are the kernel's float colour converted
+    exactly as the spec says (bit-exact against its own RGBA32F output), and
+    agree with the quantised oracle except where a float sits within the
+    kernel-vs-oracle difference of a rounding boundary."""
+    import torch
+    f = scenes.config("C3", 320, 180, precision=prec, pose=2)
+    ref32, _ = gpu(renderer, f)
+    g = f.copy()
+    g.params.output_format = fmt
+    out, _ = gpu(renderer, g)
+    want = quantize(ref32, fmt)
+    assert out.dtype == want.dtype
+    assert np.array_equal(out.view(np.uint8), want.view(np.uint8))
+    orc, _ = oracle.render(scenes.config("C3", 320, 180, pose=2))
+    oq = quantize(orc, fmt).astype(np.float64)
+    diff = np.abs(out.astype(np.float64) - oq)
+    lsb = 1.0 if fmt == abi.FORMAT_RGBA8 else 1e-3
+    assert (diff.max(axis=-1) > 0).mean() < 1e-3 and diff.max() <= max(lsb, 5e-3)
+    # the multi-device scatter handles the narrow formats too
+    world = 3
+    stride = R.owned_rows(180, R.tiling(0, world))
+    parts = torch.zeros((world * stride, 320, 4), dtype=R.torch_dtype(fmt),
+                        device=renderer.device)
+    for r in range(world):
+        t = R.tiling(r, world)
+        n = R.owned_rows(180, t)
+        renderer.render(g, t, out=parts[r * stride:r * stride + n])
+    frame = renderer.deinterleave(parts, world, stride, 320, 180)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().view(np.uint8), out.view(np.uint8))
+
+
 def test_write_results():
     out = Path("gpurun_out")
     out.mkdir(exist_ok=True)
     (out / "parity_results.json").write_text(json.dumps(RESULTS, indent=1, sort_keys=True))
+
+
+def read_ppm(path):
+    data = Path(path).read_bytes()
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"P6"
+    w, h = map(int, parts[1].split())
+    return np.frombuffer(parts[3], dtype=np.uint8).reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("scene_name,cfg", [("ref", "REF"), ("csg8", "C3")])
+def test_cpp_host_program(renderer, tmp_path, scene_name, cfg):
+    """examples/sdf_main.cpp (C++ API in include/sdf3d.hpp) renders the same
+    frame as the Python path; its PPM is the clamped 8-bit image."""
+    import subprocess
+    exe = Path(__file__).resolve().parent.parent / "sdf3d_amd" / "bin" / "sdf_main"
+    assert exe.exists(), "build() must produce sdf3d_amd/bin/sdf_main"
+    out = tmp_path / "f.ppm"
+    r = subprocess.run([str(exe), "160", "90", "2", str(out), scene_name], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    img = read_ppm(out)
+    f = scenes.config(cfg, 160, 90, precision=abi.PRECISION_FAST)
+    scenes.set_view(f, scenes.orbit_view(180.0, 0.0))     # frame 1 of 2: yaw 180
+    rgba, _ = gpu(renderer, f, steps=False)
+    want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
+    assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
