@@ -244,8 +244,11 @@ def test_output_formats(renderer, fmt, prec):
     orc, _ = oracle.render(scenes.config("C3", 320, 180, pose=2))
     oq = quantize(orc, fmt).astype(np.float64)
     diff = np.abs(out.astype(np.float64) - oq)
+    # one LSB at most; how often a boundary is crossed depends on the float
+    # difference (exact: ~1e-7, fast: ~1e-5 against an fp16 step of ~5e-4)
     lsb = 1.0 if fmt == abi.FORMAT_RGBA8 else 1e-3
-    assert (diff.max(axis=-1) > 0).mean() < 1e-3 and diff.max() <= max(lsb, 5e-3)
+    frac = 1e-3 if prec == abi.PRECISION_EXACT else 2e-2
+    assert (diff.max(axis=-1) > 0).mean() < frac and diff.max() <= max(lsb, 5e-3)
     # the multi-device scatter handles the narrow formats too
     world = 3
     stride = R.owned_rows(180, R.tiling(0, world))
