@@ -56,7 +56,10 @@ def parse():
     ap.add_argument("--precision", default="fast", choices=["fast", "exact"])
     ap.add_argument("--pose", type=int, default=0)
     ap.add_argument("--format", default="rgba32f", choices=["rgba32f", "rgba16f", "rgba8"],
-                    help="framebuffer format written by the kernel and gathered (N>1)")
+                    help="framebuffer format of the assembled frame")
+    ap.add_argument("--wire", default="auto", choices=["auto", "rgba", "rgb32f"],
+                    help="N>1: what ranks send; auto = rgb32f (lossless, alpha restored on "
+                         "rank 0) for rgba32f frames, else the frame format")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-stride", type=int, default=4,
                     help="CPU baseline renders every k-th 8-row block of the frame")
@@ -141,6 +144,13 @@ def main():
     prec = abi.PRECISION_FAST if args.precision == "fast" else abi.PRECISION_EXACT
     frame = scenes.config(args.config, precision=prec, pose=args.pose)
     frame.params.output_format = abi.FORMAT_NAMES[args.format]
+    wire = args.wire
+    if wire == "auto":
+        wire = "rgb32f" if (world > 1 and args.format == "rgba32f") else "rgba"
+    if wire == "rgb32f":
+        if args.format != "rgba32f":
+            sys.exit("--wire rgb32f needs --format rgba32f")
+        frame.params.output_format = abi.FORMAT_RGB32F   # ranks render RGB, root expands
     W, H = frame.params.width, frame.params.height
     rd = Renderer(dev)
     t = R.tiling(rank, world, 8)
@@ -154,7 +164,8 @@ def main():
 
     drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
                       dist=dist if world > 1 else None,
-                      dtype=R.torch_dtype(frame.params.output_format))
+                      dtype=R.torch_dtype(frame.params.output_format),
+                      wire_channels=R.channels(frame.params.output_format))
     k_steps = args.steps + args.warmup
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
@@ -195,7 +206,7 @@ def main():
             "config": {"workload": f"{args.config}: {frame.meta['description']}",
                        "width": W, "height": H, "max_steps": frame.params.max_steps,
                        "precision": args.precision, "pose": args.pose,
-                       "format": args.format,
+                       "format": args.format, "wire": wire if world > 1 else None,
                        "tiling": "8-row interleaved blocks" if world > 1 else "whole frame",
                        "gather": "RCCL gather to rank 0 + sdf_deinterleave" if world > 1
                        else None},

@@ -183,11 +183,16 @@ typedef struct {
  *   RGBA16F  IEEE half, round to nearest even.
  *   RGBA8    what the reference's RGBA8 window shows (main.cpp:95-96):
  *            u8 = trunc(min(max(c, 0), 1) * 255 + 0.5), NaN -> 0, no
- *            multiply-add fusion.                                          */
+ *            multiply-add fusion.
+ *   RGB32F   RGBA32F without the alpha channel, which the shader always
+ *            writes as 1.0 (voxel_fragment.frag:210): a lossless 12-byte
+ *            wire format for multi-device frames; sdf_deinterleave expands
+ *            it to an RGBA32F frame with alpha = 1.                        */
 typedef enum {
   SDF_FORMAT_RGBA32F = 0,
   SDF_FORMAT_RGBA16F = 1,
-  SDF_FORMAT_RGBA8 = 2
+  SDF_FORMAT_RGBA8 = 2,
+  SDF_FORMAT_RGB32F = 3
 } sdf_format;
 
 typedef enum {
@@ -228,7 +233,7 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera,
  * negative SDF_E* code. */
 int sdf_owned_rows(int32_t height, const sdf_tiling* tiling);
 
-/* Bytes per pixel of a sdf_format (16, 8, 4), or a negative SDF_E* code. */
+/* Bytes per pixel of a sdf_format (16, 8, 4, 12), or a negative SDF_E* code. */
 int sdf_format_bytes(int32_t format);
 
 /* Render the rows owned by `tiling` (NULL = whole frame) into `rgba`
@@ -245,8 +250,8 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera,
 /* Scatter `nparts` packed row-block buffers (part r = rank r's output for
  * tiling {block_rows, r, nparts}), laid out back to back in `parts` with a
  * pitch of `part_stride_rows` rows each, into the full frame `frame`
- * (height * width pixels of `format`).  Device pointers; asynchronous on
- * `stream`. */
+ * (height * width pixels of `format`; RGB32F parts produce an RGBA32F frame
+ * with alpha = 1).  Device pointers; asynchronous on `stream`. */
 int sdf_deinterleave(const void* parts, int32_t nparts,
                      int32_t part_stride_rows, int32_t width, int32_t height,
                      int32_t block_rows, int32_t format, void* frame, void* stream);

@@ -45,4 +45,29 @@ int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int
   return (int)hipGetLastError();
 }
 
+// RGB32F parts (12 B/pixel, the lossless wire format) -> RGBA32F frame with
+// alpha = 1 (the shader's constant alpha, voxel_fragment.frag:210).
+__global__ __launch_bounds__(256) void deinterleave_rgb_rows(const float* __restrict__ parts,
+                                                             int nparts, int part_stride_rows,
+                                                             int width, int block_rows,
+                                                             float4* __restrict__ frame) {
+  const int y = blockIdx.x;
+  const int b = y / block_rows;
+  const int r = b % nparts;
+  const int pr = (b / nparts) * block_rows + (y - b * block_rows);
+  const float* src = parts + ((size_t)r * part_stride_rows + pr) * width * 3;
+  float4* dst = frame + (size_t)y * width;
+  for (int x = threadIdx.x; x < width; x += blockDim.x)
+    dst[x] = make_float4(src[3 * x], src[3 * x + 1], src[3 * x + 2], 1.0f);
+}
+
+int launch_deinterleave_rgb(const void* parts, int nparts, int part_stride_rows, int width,
+                            int height, int block_rows, void* frame, void* stream) {
+  if (height == 0 || width == 0) return 0;
+  hipLaunchKernelGGL(deinterleave_rgb_rows, dim3(height), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float*>(parts), nparts, part_stride_rows, width,
+                     block_rows, reinterpret_cast<float4*>(frame));
+  return (int)hipGetLastError();
+}
+
 }  // namespace sdf

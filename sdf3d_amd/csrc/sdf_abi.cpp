@@ -347,6 +347,7 @@ int sdf_format_bytes(int32_t format) {
     case SDF_FORMAT_RGBA32F: return 16;
     case SDF_FORMAT_RGBA16F: return 8;
     case SDF_FORMAT_RGBA8: return 4;
+    case SDF_FORMAT_RGB32F: return 12;
     default: return SDF_E_INVALID_ARG;
   }
 }
@@ -438,8 +439,12 @@ int sdf_deinterleave(const void* parts, int32_t nparts, int32_t part_stride_rows
     const sdf_tiling t = {block_rows, r, nparts, 0};
     if (count_rows(height, t) > part_stride_rows) return SDF_E_INVALID_ARG;
   }
-  const int err = sdf::launch_deinterleave(parts, nparts, part_stride_rows, width * bpp, height,
-                                           block_rows, frame, stream);
+  const int err =
+      format == SDF_FORMAT_RGB32F
+          ? sdf::launch_deinterleave_rgb(parts, nparts, part_stride_rows, width, height,
+                                         block_rows, frame, stream)
+          : sdf::launch_deinterleave(parts, nparts, part_stride_rows, width * bpp, height,
+                                     block_rows, frame, stream);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 

@@ -53,7 +53,7 @@ def deinterleave_index(height: int, world: int, stride: int, block_rows: int = 8
 class FrameDriver:
     def __init__(self, width: int, height: int, rank: int, world: int, device,
                  render_fn: Callable, deinterleave_fn: Callable, block_rows: int = 8,
-                 nbuf: int = 2, dist=None, dtype=None):
+                 nbuf: int = 2, dist=None, dtype=None, wire_channels: int = 4):
         import torch
         self.torch = torch
         self.W, self.H = width, height
@@ -69,11 +69,12 @@ class FrameDriver:
         self.nbuf = nbuf if world > 1 else 1
         dtype = dtype or torch.float32   # the framebuffer format on the wire
         mk = lambda *shape: torch.empty(shape, dtype=dtype, device=device)  # noqa: E731
-        self.local = [mk(self.stride, width, 4) for _ in range(self.nbuf)]
+        wc = wire_channels   # 3: RGB32F wire, alpha restored by the deinterleave
+        self.local = [mk(self.stride, width, wc if world > 1 else 4) for _ in range(self.nbuf)]
         self.works = [None] * self.nbuf
         self.root = rank == 0
         if world > 1 and self.root:
-            self.gathered = [mk(world * self.stride, width, 4) for _ in range(self.nbuf)]
+            self.gathered = [mk(world * self.stride, width, wc) for _ in range(self.nbuf)]
             self.frames = [mk(height, width, 4) for _ in range(self.nbuf)]
             self.deint_done = [None] * self.nbuf
         self.stream = torch.cuda.current_stream(device) if self.gpu else None
@@ -138,8 +139,14 @@ class FrameDriver:
 
 
 def deinterleave_torch(parts, world, stride, W, H, B, out, stream=None):
-    """CPU stand-in for sdf_deinterleave (index math of deinterleave.hip)."""
+    """CPU stand-in for sdf_deinterleave (index math of deinterleave.hip;
+    3-channel parts get alpha = 1)."""
     import torch
     idx = torch.as_tensor(deinterleave_index(H, world, stride, B), device=parts.device)
-    out.copy_(parts.index_select(0, idx))
+    rows = parts.index_select(0, idx)
+    if rows.shape[-1] == 3:
+        out[..., :3].copy_(rows)
+        out[..., 3] = 1.0
+    else:
+        out.copy_(rows)
     return out

@@ -30,10 +30,14 @@ def owned_rows(height: int, t: abi.sdf_tiling | None = None) -> int:
 
 
 def torch_dtype(fmt: int):
-    """torch element type of a framebuffer format (4 channels per pixel)."""
+    """torch element type of a framebuffer format."""
     import torch
     return {abi.FORMAT_RGBA32F: torch.float32, abi.FORMAT_RGBA16F: torch.float16,
-            abi.FORMAT_RGBA8: torch.uint8}[fmt]
+            abi.FORMAT_RGBA8: torch.uint8, abi.FORMAT_RGB32F: torch.float32}[fmt]
+
+
+def channels(fmt: int) -> int:
+    return abi.FORMAT_CHANNELS[fmt]
 
 
 class Renderer:
@@ -57,7 +61,8 @@ class Renderer:
     def alloc(self, frame: Frame, t: abi.sdf_tiling | None = None, steps: bool = False):
         rows = owned_rows(frame.params.height, t)
         w = frame.params.width
-        rgba = self.torch.empty((rows, w, 4), dtype=torch_dtype(frame.params.output_format),
+        fmt = frame.params.output_format
+        rgba = self.torch.empty((rows, w, channels(fmt)), dtype=torch_dtype(fmt),
                                 device=self.device)
         st = (self.torch.empty((rows, w, 2), dtype=self.torch.int32, device=self.device)
               if steps else None)
@@ -80,9 +85,10 @@ class Renderer:
         if isinstance(steps, torch.Tensor):
             st = steps
         dt = torch_dtype(frame.params.output_format)
-        if tuple(rgba.shape) != (rows, w, 4) or rgba.dtype != dt \
+        ch = channels(frame.params.output_format)
+        if tuple(rgba.shape) != (rows, w, ch) or rgba.dtype != dt \
                 or not rgba.is_contiguous() or rgba.device != self.device:
-            raise ValueError(f"rgba must be a contiguous {dt} ({rows}, {w}, 4) tensor "
+            raise ValueError(f"rgba must be a contiguous {dt} ({rows}, {w}, {ch}) tensor "
                              f"on {self.device}")
         if st is not None and (tuple(st.shape) != (rows, w, 2) or st.dtype != torch.int32
                                or not st.is_contiguous()):
@@ -107,11 +113,15 @@ class Renderer:
         if fmt is None:
             fmt = {torch.float32: abi.FORMAT_RGBA32F, torch.float16: abi.FORMAT_RGBA16F,
                    torch.uint8: abi.FORMAT_RGBA8}[parts.dtype]
+            if parts.shape[-1] == 3:
+                fmt = abi.FORMAT_RGB32F
         if out is None:
             out = torch.empty((height, width, 4), dtype=torch_dtype(fmt), device=self.device)
-        if parts.numel() < nparts * part_stride_rows * width * 4 or not parts.is_contiguous() \
-                or parts.dtype != torch_dtype(fmt) or out.dtype != parts.dtype:
-            raise ValueError("parts buffer too small, not contiguous or of another format")
+        if parts.numel() < nparts * part_stride_rows * width * channels(fmt) \
+                or not parts.is_contiguous() or parts.dtype != torch_dtype(fmt) \
+                or out.dtype != parts.dtype or tuple(out.shape) != (height, width, 4) \
+                or not out.is_contiguous():
+            raise ValueError("parts/frame buffers of the wrong size, layout or format")
         with torch.cuda.device(self.device):
             rc = self.lib.sdf_deinterleave(C.c_void_p(parts.data_ptr()), nparts,
                                            part_stride_rows, width, height, block_rows, fmt,

@@ -22,10 +22,13 @@ MAX_ERR = 0.05
 def quantize(rgba, fmt):
     """Reference conversion of float RGBA to a framebuffer format (sdf_abi.h
     sdf_format): 0 rgba32f, 1 rgba16f (round to nearest even), 2 rgba8
-    (trunc(min(max(c,0),1) * 255 + 0.5), NaN -> 0, fp32 mul then add)."""
+    (trunc(min(max(c,0),1) * 255 + 0.5), NaN -> 0, fp32 mul then add),
+    3 rgb32f (alpha dropped)."""
     a = np.asarray(rgba, dtype=np.float32)
     if fmt == 0:
         return a
+    if fmt == 3:                       # RGB32F: alpha (always 1) dropped
+        return np.ascontiguousarray(a[..., :3])
     if fmt == 1:
         return a.astype(np.float16)
     q = np.fmin(np.fmax(a, np.float32(0)), np.float32(1))   # fmax/fmin drop NaN -> 0

@@ -225,7 +225,7 @@ def test_invalid_arguments_are_rejected_on_device(renderer):
         renderer.render(f, out=out)
 
 
-@pytest.mark.parametrize("fmt", [abi.FORMAT_RGBA16F, abi.FORMAT_RGBA8])
+@pytest.mark.parametrize("fmt", [abi.FORMAT_RGBA16F, abi.FORMAT_RGBA8, abi.FORMAT_RGB32F])
 @pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
 def test_output_formats(renderer, fmt, prec):
     """RGBA16F / RGBA8 framebuffers are the kernel's float colour converted
@@ -252,7 +252,7 @@ def test_output_formats(renderer, fmt, prec):
     # the multi-device scatter handles the narrow formats too
     world = 3
     stride = R.owned_rows(180, R.tiling(0, world))
-    parts = torch.zeros((world * stride, 320, 4), dtype=R.torch_dtype(fmt),
+    parts = torch.zeros((world * stride, 320, R.channels(fmt)), dtype=R.torch_dtype(fmt),
                         device=renderer.device)
     for r in range(world):
         t = R.tiling(r, world)
@@ -260,7 +260,9 @@ def test_output_formats(renderer, fmt, prec):
         renderer.render(g, t, out=parts[r * stride:r * stride + n])
     frame = renderer.deinterleave(parts, world, stride, 320, 180)
     torch.cuda.synchronize()
-    assert np.array_equal(frame.cpu().numpy().view(np.uint8), out.view(np.uint8))
+    # RGB32F wire parts come back as the RGBA32F frame (alpha restored = 1)
+    full = ref32 if fmt == abi.FORMAT_RGB32F else out
+    assert np.array_equal(frame.cpu().numpy().view(np.uint8), full.view(np.uint8))
 
 
 def test_write_results():

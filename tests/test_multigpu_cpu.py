@@ -27,7 +27,7 @@ def frame_for(step):
     return scenes.config("C3", 72, 43, pose=step % 4)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, wire_channels=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -36,11 +36,12 @@ def _worker(rank, world, port, q):
         def render_fn(out, stream):
             f = frame_for(step_box[0])
             rgba, _ = oracle.render(f, R.tiling(rank, world, 8), nthreads=1)
-            out.copy_(torch.from_numpy(rgba))
+            out.copy_(torch.from_numpy(rgba[..., :out.shape[-1]].copy()))
 
         f0 = frame_for(0)
         drv = FrameDriver(f0.params.width, f0.params.height, rank, world, torch.device("cpu"),
-                          render_fn, deinterleave_torch, dist=dist)
+                          render_fn, deinterleave_torch, dist=dist,
+                          wire_channels=wire_channels)
         frames = []
         for i in range(5):
             step_box[0] = i
@@ -58,12 +59,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_frame_driver_gloo(world):
+@pytest.mark.parametrize("world,wire", [(2, 4), (3, 4), (2, 3)])
+def test_frame_driver_gloo(world, wire):
+    """wire = 3: the lossless RGB32F wire format (alpha restored on rank 0)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire)) for r in range(world)]
     for p in procs:
         p.start()
     frames = q.get(timeout=240)
