@@ -113,7 +113,7 @@ def test_render_rejects_null_output():
                         C.byref(f.material), C.byref(f.params), None, None, None, None)
     assert rc == abi.SDF_E_INVALID_ARG
     assert lib.sdf_deinterleave(None, 1, 1, 1, 1, 8, 0, None, None) == abi.SDF_E_INVALID_ARG
-    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3)] == [16, 8, 4, abi.SDF_E_INVALID_ARG]
+    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3, 4)] == [16, 8, 4, 12, abi.SDF_E_INVALID_ARG]
 
 
 @pytest.mark.parametrize("height", [1, 7, 8, 9, 23, 600, 1080, 2160])
