@@ -64,6 +64,12 @@ def parse():
     ap.add_argument("--cpu-sample-stride", type=int, default=4,
                     help="CPU baseline renders every k-th 8-row block of the frame")
     ap.add_argument("--cpu-frames", type=int, default=5)
+    ap.add_argument("--no-verify", action="store_true",
+                    help="N>1: skip the post-run check that rank 0's assembled frame equals "
+                         "a single-device render bit for bit")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to "
+                         "rehearse several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -136,10 +142,15 @@ def main():
     from sdf3d_amd import renderer as R
     from sdf3d_amd.multigpu import FrameDriver
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % ndev if args.backend == "gloo" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     prec = abi.PRECISION_FAST if args.precision == "fast" else abi.PRECISION_EXACT
     frame = scenes.config(args.config, precision=prec, pose=args.pose)
@@ -191,6 +202,18 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
+    verified = None
+    if world > 1 and not args.no_verify and rank == 0:
+        # outside the timed region: the assembled frame of the last step must
+        # equal a whole-frame render on this device (pixels are independent)
+        whole = scenes.config(args.config, precision=prec, pose=args.pose)
+        whole.params.output_format = abi.FORMAT_NAMES[args.format]
+        ref, _ = rd.render(whole)
+        got = drv.frame(k_steps - 1)
+        torch.cuda.synchronize(dev)
+        verified = bool(torch.equal(got.view(torch.uint8), ref.view(torch.uint8)))
+        log(f"[bench] assembled frame == single-device frame: {verified}")
+
     kernel_ms = [ev0[i].elapsed_time(ev1[i]) for i in range(args.warmup, k_steps)]
     kavg_ms = sum(kernel_ms) / len(kernel_ms)
     flops = rank_flops(frame, t, args.pose)
@@ -208,9 +231,10 @@ def main():
                        "precision": args.precision, "pose": args.pose,
                        "format": args.format, "wire": wire if world > 1 else None,
                        "tiling": "8-row interleaved blocks" if world > 1 else "whole frame",
-                       "gather": "RCCL gather to rank 0 + sdf_deinterleave" if world > 1
-                       else None},
+                       "gather": (f"{'RCCL' if args.backend == 'nccl' else 'gloo'} gather to "
+                                  "rank 0 + sdf_deinterleave") if world > 1 else None},
             "fps": round(args.steps / elapsed, 2),
+            "frame_verified": verified,
             "kernel_ms": round(kavg_ms, 4),
         }
         if flops is not None:

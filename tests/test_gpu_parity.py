@@ -241,14 +241,19 @@ def test_output_formats(renderer, fmt, prec):
     want = quantize(ref32, fmt)
     assert out.dtype == want.dtype
     assert np.array_equal(out.view(np.uint8), want.view(np.uint8))
-    orc, _ = oracle.render(scenes.config("C3", 320, 180, pose=2))
-    oq = quantize(orc, fmt).astype(np.float64)
-    diff = np.abs(out.astype(np.float64) - oq)
-    # one LSB at most; how often a boundary is crossed depends on the float
-    # difference (exact: ~1e-7, fast: ~1e-5 against an fp16 step of ~5e-4)
-    lsb = 1.0 if fmt == abi.FORMAT_RGBA8 else 1e-3
-    frac = 1e-3 if prec == abi.PRECISION_EXACT else 2e-2
-    assert (diff.max(axis=-1) > 0).mean() < frac and diff.max() <= max(lsb, 5e-3)
+    orc, ost = oracle.render(scenes.config("C3", 320, 180, pose=2))
+    if fmt == abi.FORMAT_RGB32F:
+        # a float format: the RGBA32F parity policy applies (alpha is 1)
+        rgba = np.concatenate([out, np.ones_like(out[..., :1])], -1)
+        _, gst = gpu(renderer, f)
+        assert_parity(report(rgba, gst, orc, ost), what="rgb32f")
+    else:
+        diff = np.abs(out.astype(np.float64) - quantize(orc, fmt).astype(np.float64))
+        # one LSB at most; how often a boundary is crossed depends on the float
+        # difference (exact: ~1e-7, fast: ~1e-5 against an fp16 step of ~5e-4)
+        lsb = 1.0 if fmt == abi.FORMAT_RGBA8 else 1e-3
+        frac = 1e-3 if prec == abi.PRECISION_EXACT else 2e-2
+        assert (diff.max(axis=-1) > 0).mean() < frac and diff.max() <= max(lsb, 5e-3)
     # the multi-device scatter handles the narrow formats too
     world = 3
     stride = R.owned_rows(180, R.tiling(0, world))
