@@ -256,6 +256,15 @@ int sdf_deinterleave(const void* parts, int32_t nparts,
                      int32_t part_stride_rows, int32_t width, int32_t height,
                      int32_t block_rows, int32_t format, void* frame, void* stream);
 
+/* Debug view of the `steps` output of sdf_render: `count` int2 entries
+ * (primary, shadow) -> colours of `format`, with which = 0 (primary), 1
+ * (shadow) or 2 (their sum), intensity = steps / max_steps mapped through the
+ * Turbo colormap the reference ships unused (Code/kernel/utilities.cl:7-284;
+ * index round(255 * intensity) clamped to [0, 255], alpha 1).  Device
+ * pointers; asynchronous on `stream`. */
+int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_steps,
+                int32_t format, void* out, void* stream);
+
 /* Short description of a status code. */
 const char* sdf_strerror(int code);
 

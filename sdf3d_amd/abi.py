@@ -103,6 +103,8 @@ SIGNATURES = {
     "sdf_deinterleave": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_format_bytes": (C.c_int, [C.c_int32]),
+    "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                              C.c_void_p, C.c_void_p]),
     "sdf_strerror": (C.c_char_p, [C.c_int]),
 }
 

@@ -32,6 +32,7 @@ UNITS = [
     ("render_exact.hip", ["-ffp-contract=off"]),
     ("render_fast.hip", ["-ffp-contract=fast"]),
     ("deinterleave.hip", []),
+    ("heatmap.hip", []),
     ("sdf_abi.cpp", ["-ffp-contract=off", "-x", "hip"]),
 ]
 HEADERS = [CSRC / "kernel_args.h", CSRC / "render_kernel.inc", ROOT / "include" / "sdf_abi.h"]

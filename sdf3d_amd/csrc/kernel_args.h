@@ -59,6 +59,8 @@ int launch_render_exact(const KernelArgs& a, int variant, void* stream);
 int launch_render_fast(const KernelArgs& a, int variant, void* stream);
 int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int row_bytes,
                         int height, int block_rows, void* frame, void* stream);
+int launch_heatmap(const int32_t* steps, int count, int which, int max_steps, int format,
+                   void* out, void* stream);
 int launch_deinterleave_rgb(const void* parts, int nparts, int part_stride_rows, int width,
                             int height, int block_rows, void* frame, void* stream);
 

@@ -448,6 +448,16 @@ int sdf_deinterleave(const void* parts, int32_t nparts, int32_t part_stride_rows
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 
+int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_steps,
+                int32_t format, void* out, void* stream) {
+  if (count < 0 || which < 0 || which > 2 || max_steps < 0 || sdf_format_bytes(format) < 0)
+    return SDF_E_INVALID_ARG;
+  if (count == 0) return SDF_OK;
+  if (!steps || !out) return SDF_E_INVALID_ARG;
+  const int err = sdf::launch_heatmap(steps, count, which, max_steps, format, out, stream);
+  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+}
+
 const char* sdf_strerror(int code) {
   switch (code) {
     case SDF_OK: return "success";

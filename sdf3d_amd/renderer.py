@@ -104,6 +104,22 @@ class Renderer:
         abi.check(rc, "sdf_render")
         return rgba, st
 
+    def heatmap(self, steps, which: int = 0, max_steps: int = 128, fmt: int = abi.FORMAT_RGBA8,
+                out=None, stream=None):
+        """Turbo-coloured view of a `steps` tensor (rows, W, 2) from render()."""
+        torch = self.torch
+        if steps.dtype != torch.int32 or steps.shape[-1] != 2 or not steps.is_contiguous():
+            raise ValueError("steps must be a contiguous int32 (..., 2) tensor")
+        count = steps.numel() // 2
+        if out is None:
+            out = torch.empty((*steps.shape[:-1], channels(fmt)), dtype=torch_dtype(fmt),
+                              device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdf_heatmap(C.c_void_p(steps.data_ptr()), count, which, max_steps,
+                                      fmt, C.c_void_p(out.data_ptr()), self._stream(stream))
+        abi.check(rc, "sdf_heatmap")
+        return out
+
     def deinterleave(self, parts, nparts: int, part_stride_rows: int, width: int,
                      height: int, block_rows: int = 8, out=None, stream=None,
                      fmt: int | None = None):

@@ -301,3 +301,58 @@ def test_cpp_host_program(renderer, tmp_path, scene_name, cfg):
     rgba, _ = gpu(renderer, f, steps=False)
     want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
     assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
+
+
+def test_multirank_bench_rehearsal(renderer, tmp_path):
+    """bench.py with 2 ranks sharing this GPU (gloo backend; RCCL needs one GPU
+    per rank): the FrameDriver's GPU path -- RGB32F wire, async gather,
+    side-stream sdf_deinterleave -- assembles frames bit-identical to a
+    single-device render."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = Path(__file__).resolve().parent.parent
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(root / "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--backend", "gloo",
+           "--config", "C3"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["frame_verified"] is True and d["config"]["wire"] == "rgb32f"
+
+
+def turbo_ref(steps, which, max_steps):
+    """numpy statement of sdf_heatmap (heatmap.hip)."""
+    s = steps.astype(np.int64)
+    n = s[..., 0] if which == 0 else (s[..., 1] if which == 1 else s[..., 0] + s[..., 1])
+    t = (n.astype(np.float32) * np.float32(1.0 / max_steps)).astype(np.float32)
+    idx = np.clip(np.rint(np.float32(255) * t), 0, 255)
+    x = (idx / 255.0).astype(np.float64)
+    c = np.stack([
+        0.13572138 + 4.61539260 * x - 42.66032258 * x**2 + 132.13108234 * x**3
+        - 152.94239396 * x**4 + 59.28637943 * x**5,
+        0.09140261 + 2.19418839 * x + 4.84296658 * x**2 - 14.18503333 * x**3
+        + 4.27729857 * x**4 + 2.82956604 * x**5,
+        0.10667330 + 12.64194608 * x - 60.58204836 * x**2 + 110.36276771 * x**3
+        - 89.90310912 * x**4 + 27.34824973 * x**5], -1)
+    c = np.clip(c, 0, 1)
+    return np.concatenate([c, np.ones_like(c[..., :1])], -1)
+
+
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_heatmap(renderer, which):
+    import torch
+    f = scenes.config("C3", 256, 144, precision=abi.PRECISION_FAST, pose=1)
+    _, st = renderer.render(f, steps=True)
+    h32 = renderer.heatmap(st, which, f.params.max_steps, abi.FORMAT_RGBA32F)
+    h8 = renderer.heatmap(st, which, f.params.max_steps, abi.FORMAT_RGBA8)
+    torch.cuda.synchronize()
+    want = turbo_ref(st.cpu().numpy(), which, f.params.max_steps)
+    assert np.abs(h32.cpu().numpy() - want).max() < 1e-4
+    assert np.array_equal(h8.cpu().numpy(), quantize(h32.cpu().numpy(), abi.FORMAT_RGBA8))
