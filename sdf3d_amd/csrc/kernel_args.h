@@ -100,6 +100,9 @@ constexpr int kPrimPlaneY = 7;
 constexpr float kCullAbs = 1e-4f;
 constexpr float kCullRel = 1e-5f;
 constexpr float kCullScale = 1.0f / (1.0f - kCullRel);
+// path lengths used by cached bounds are scaled up by this factor so that
+// unit directions normalised in fp32 (|dir| <= 1 + 2^-22) stay conservative
+constexpr float kPathScale = 1.000002f;
 constexpr bool cullable(int kind, int op) {
   return kind != SDF_PRIM_PLANE && kind != kPrimPlaneY &&
          (op == SDF_OP_SMOOTH_UNION || (op == SDF_OP_UNION && kind != SDF_PRIM_SPHERE));
