@@ -197,7 +197,10 @@ typedef enum {
 
 typedef enum {
   SDF_DISPATCH_AUTO = 0,       /* specialised kernel if the scene matches one  */
-  SDF_DISPATCH_GENERIC = 1     /* always the generic primitive-list kernel     */
+  SDF_DISPATCH_GENERIC = 1,    /* always the generic primitive-list kernel     */
+  SDF_DISPATCH_UNCULLED = 2    /* generic kernel evaluating every primitive at
+                                  every point (no bounding-volume culling): the
+                                  straight restatement, for cross-checks       */
 } sdf_dispatch;
 
 /* Which rows of the frame a call renders.  Rows are grouped into blocks of

@@ -33,7 +33,7 @@ SCENE_PRIMITIVES, SCENE_MANDELBULB = 0, 1
 FLAG_SHADOW, FLAG_AO = 0x1, 0x2
 NORMAL_CENTRAL, NORMAL_TETRA = 0, 1
 PRECISION_EXACT, PRECISION_FAST = 0, 1
-DISPATCH_AUTO, DISPATCH_GENERIC = 0, 1
+DISPATCH_AUTO, DISPATCH_GENERIC, DISPATCH_UNCULLED = 0, 1, 2
 FORMAT_RGBA32F, FORMAT_RGBA16F, FORMAT_RGBA8, FORMAT_RGB32F = 0, 1, 2, 3
 FORMAT_NAMES = {"rgba32f": FORMAT_RGBA32F, "rgba16f": FORMAT_RGBA16F, "rgba8": FORMAT_RGBA8,
                 "rgb32f": FORMAT_RGB32F}

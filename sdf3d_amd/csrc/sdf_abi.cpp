@@ -307,7 +307,7 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
     return SDF_E_INVALID_ARG;
   if (p.precision != SDF_PRECISION_EXACT && p.precision != SDF_PRECISION_FAST)
     return SDF_E_INVALID_ARG;
-  if (p.dispatch != SDF_DISPATCH_AUTO && p.dispatch != SDF_DISPATCH_GENERIC)
+  if (p.dispatch < SDF_DISPATCH_AUTO || p.dispatch > SDF_DISPATCH_UNCULLED)
     return SDF_E_INVALID_ARG;
   if (sdf_format_bytes(p.output_format) < 0) return SDF_E_INVALID_ARG;
   if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > 64)) return SDF_E_INVALID_ARG;
@@ -418,9 +418,10 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.rgba = rgba;
   a.steps = steps;
 
-  const int variant = params->dispatch == SDF_DISPATCH_GENERIC && scene->kind == SDF_SCENE_PRIMITIVES
-                            ? sdf::kVariantGeneric
-                            : sdf::select_variant(*scene);
+  const bool generic = params->dispatch != SDF_DISPATCH_AUTO &&
+                       scene->kind == SDF_SCENE_PRIMITIVES;
+  if (params->dispatch == SDF_DISPATCH_UNCULLED) a.cluster_first = a.prim_count;
+  const int variant = generic ? sdf::kVariantGeneric : sdf::select_variant(*scene);
   const int err = params->precision == SDF_PRECISION_FAST
                       ? sdf::launch_render_fast(a, variant, stream)
                       : sdf::launch_render_exact(a, variant, stream);

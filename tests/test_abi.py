@@ -83,6 +83,7 @@ def test_validate_accepts_all_configs():
     lambda f: setattr(f.params, "precision", 9),
     lambda f: setattr(f.params, "output_format", 7),
     lambda f: setattr(f.params, "dispatch", 3),
+    lambda f: setattr(f.params, "dispatch", -1),
     lambda f: setattr(f.params, "eps", float("nan")),
     lambda f: setattr(f.scene, "count", abi.SDF_MAX_PRIMS + 1),
     lambda f: setattr(f.scene.prims[0], "kind", 99),

@@ -78,7 +78,7 @@ def test_specialised_matches_generic(renderer, cfg, pose):
         f = scenes.config(cfg, 192, 108, precision=prec, pose=pose)
         a, sa = gpu(renderer, f)
         g = f.copy()
-        g.params.dispatch = abi.DISPATCH_GENERIC
+        g.params.dispatch = abi.DISPATCH_UNCULLED
         b, sb = gpu(renderer, g)
         if prec == abi.PRECISION_EXACT or cfg == "C5":
             assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(sa, sb)
@@ -356,3 +356,66 @@ def test_heatmap(renderer, which):
     want = turbo_ref(st.cpu().numpy(), which, f.params.max_steps)
     assert np.abs(h32.cpu().numpy() - want).max() < 1e-4
     assert np.array_equal(h8.cpu().numpy(), quantize(h32.cpu().numpy(), abi.FORMAT_RGBA8))
+
+
+def random_csg8(rng, spread, kmax):
+    """A scene with the CSG8 signature (so the culled FixedScene variant runs)
+    but random sizes, positions and blend radii."""
+    f = scenes.config("C3", 160, 96)
+    s = f.scene
+    u = lambda a, b: float(rng.uniform(a, b))  # noqa: E731
+    c = lambda: (u(-spread, spread), u(-0.2, spread), u(-spread, spread))  # noqa: E731
+    s.prims[0].p[3] = u(-0.3, 0.3)                                  # plane offset
+    for i in range(1, 8):
+        pr = s.prims[i]
+        pr.k = u(1e-3, kmax)
+        x, y, z = c()
+        pr.p[0], pr.p[1], pr.p[2] = x, y, z
+        kind = pr.kind
+        if kind == abi.PRIM_SPHERE:
+            pr.p[3] = u(0.01, 0.6)
+        elif kind in (abi.PRIM_BOX, abi.PRIM_ROUND_BOX):
+            pr.p[3], pr.p[4], pr.p[5] = u(0.02, 0.5), u(0.02, 0.5), u(0.02, 0.5)
+            if kind == abi.PRIM_ROUND_BOX:
+                pr.p[6] = u(0.0, 0.5) * min(pr.p[3], pr.p[4], pr.p[5])
+        elif kind == abi.PRIM_TORUS:
+            pr.p[3], pr.p[4] = u(0.05, 0.5), u(0.01, 0.2)
+        elif kind == abi.PRIM_CAPSULE:
+            pr.p[3], pr.p[4], pr.p[5] = c()
+            pr.p[6] = u(0.01, 0.3)
+        elif kind == abi.PRIM_CYLINDER:
+            pr.p[3], pr.p[4] = u(0.02, 0.4), u(0.02, 0.6)
+    return f
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_culling_exact_on_random_scenes(renderer, seed):
+    """The culled fixed-scene kernel equals the unculled generic kernel bit for
+    bit (exact precision), step counts included, for random parameters of the
+    CSG8 signature: overlapping objects, large blend radii, camera inside."""
+    rng = np.random.default_rng(seed)
+    spread = [0.5, 1.0, 2.5][seed % 3]
+    kmax = [0.05, 0.3, 1.0][(seed // 3) % 3]
+    f = random_csg8(rng, spread, kmax)
+    if seed % 4 == 3:
+        scenes.set_view(f, scenes.orbit_view(float(rng.uniform(-180, 180)),
+                                              float(rng.uniform(-20, 20))))
+    f.params.precision = abi.PRECISION_EXACT
+    a, sa = gpu(renderer, f)
+    u = f.copy()
+    u.params.dispatch = abi.DISPATCH_UNCULLED
+    b, sb = gpu(renderer, u)
+    g = f.copy()
+    g.params.dispatch = abi.DISPATCH_GENERIC          # generic kernel, culled
+    c, sc = gpu(renderer, g)
+    for x, sx in ((a, sa), (c, sc)):
+        assert np.array_equal(sx, sb)
+        assert np.array_equal(x.view(np.uint32), b.view(np.uint32))
+    # fast precision: culled vs unculled within the parity policy
+    for h in (f, u, g):
+        h.params.precision = abi.PRECISION_FAST
+    a, sa = gpu(renderer, f)
+    b, sb = gpu(renderer, u)
+    c, sc = gpu(renderer, g)
+    assert_parity(report(a, sa, b, sb), what=f"seed {seed}")
+    assert_parity(report(c, sc, b, sb), what=f"seed {seed} generic")

@@ -44,7 +44,8 @@ def main():
         variant("primary+normal", flags=0),
         variant("central_normal", normal_mode=abi.NORMAL_CENTRAL),
         variant("exact", precision=abi.PRECISION_EXACT),
-        variant("generic_unculled", dispatch=abi.DISPATCH_GENERIC),
+        variant("generic_culled", dispatch=abi.DISPATCH_GENERIC),
+        variant("unculled", dispatch=abi.DISPATCH_UNCULLED),
         variant("max_steps_1", max_steps=1, flags=0),
     ]
     _ = full
