@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true",
                     help="N>1: skip the post-run check that rank 0's assembled frame equals "
                          "a single-device render bit for bit")
+    ap.add_argument("--no-display", action="store_true",
+                    help="skip the extra RGBA8-framebuffer measurement reported beside value")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -167,40 +169,58 @@ def main():
     t = R.tiling(rank, world, 8)
     rows = R.owned_rows(H, t)
 
-    def render_fn(out, stream):
-        rd.render(frame, t, out=out, stream=stream)
+    def timed_run(fr, steps, warmup):
+        """warmup + `steps` timed frames of `fr` through a FrameDriver; returns
+        (max-over-ranks seconds, per-launch kernel ms list, driver)."""
+        def render_fn(out, stream):
+            rd.render(fr, t, out=out, stream=stream)
 
-    def deint_fn(parts, nparts, stride, w, h, b, out, stream):
-        rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
+        def deint_fn(parts, nparts, stride, w, h, b, out, stream):
+            rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
 
-    drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
-                      dist=dist if world > 1 else None,
-                      dtype=R.torch_dtype(frame.params.output_format),
-                      wire_channels=R.channels(frame.params.output_format))
-    k_steps = args.steps + args.warmup
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(k_steps)]
+        drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
+                          dist=dist if world > 1 else None,
+                          dtype=R.torch_dtype(fr.params.output_format),
+                          wire_channels=R.channels(fr.params.output_format))
+        k = steps + warmup
+        e0 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        e1 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        for i in range(warmup):
+            drv.step(i, e0[i], e1[i])
+        drv.drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(warmup, k):
+            drv.step(i, e0[i], e1[i])
+        drv.drain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            e = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el, [e0[i].elapsed_time(e1[i]) for i in range(warmup, k)], drv
 
     log(f"[bench] rank {rank}/{world} {args.config} {W}x{H} rows={rows} "
         f"precision={args.precision} warmup={args.warmup} steps={args.steps}")
-    for i in range(args.warmup):
-        drv.step(i, ev0[i], ev1[i])
-    drv.drain()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.warmup, k_steps):
-        drv.step(i, ev0[i], ev1[i])
-    drv.drain()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    elapsed, kernel_ms, drv = timed_run(frame, args.steps, args.warmup)
+    k_steps = args.steps + args.warmup
+
+    # the same workload written as the reference window's RGBA8 framebuffer:
+    # 4 B/pixel on the gather wire instead of 12 (reported beside `value`)
+    display = None
+    if args.format == "rgba32f" and not args.no_display:
+        fr8 = frame.copy()
+        fr8.params.output_format = abi.FORMAT_RGBA8
+        el8, km8, _ = timed_run(fr8, args.steps, args.warmup)
+        display = {"format": "rgba8", "value": round(W * H * args.steps / el8 / 1e6, 3),
+                   "fps": round(args.steps / el8, 2),
+                   "ms_per_step": round(el8 / args.steps * 1e3, 4),
+                   "kernel_ms": round(sum(km8) / len(km8), 4)}
 
     verified = None
     if world > 1 and not args.no_verify and rank == 0:
@@ -214,7 +234,6 @@ def main():
         verified = bool(torch.equal(got.view(torch.uint8), ref.view(torch.uint8)))
         log(f"[bench] assembled frame == single-device frame: {verified}")
 
-    kernel_ms = [ev0[i].elapsed_time(ev1[i]) for i in range(args.warmup, k_steps)]
     kavg_ms = sum(kernel_ms) / len(kernel_ms)
     flops = rank_flops(frame, t, args.pose)
 
@@ -235,6 +254,7 @@ def main():
                                   "rank 0 + sdf_deinterleave") if world > 1 else None},
             "fps": round(args.steps / elapsed, 2),
             "frame_verified": verified,
+            "display_rgba8": display,
             "kernel_ms": round(kavg_ms, 4),
         }
         if flops is not None:
