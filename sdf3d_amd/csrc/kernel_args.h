@@ -12,6 +12,8 @@
 
 namespace sdf {
 
+constexpr int kMaxAoTaps = 64;
+
 struct KernelArgs {
   // camera (hoisted uniforms)
   float inv_view[16];   // inverse(V_mat), column-major
@@ -32,6 +34,8 @@ struct KernelArgs {
   int32_t flags, normal_mode, format;
   int32_t ao_taps;
   float ao_step, ao_base, ao_falloff, ao_strength;
+  float ao_h[kMaxAoTaps];  // tap heights base + step * i / (taps - 1), host fp32
+  float inv_width, inv_height;  // fast precision quad mapping
   // tiling
   int32_t block_rows, first_block, block_stride, rows;
   // scene

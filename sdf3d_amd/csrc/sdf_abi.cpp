@@ -310,7 +310,8 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   if (p.dispatch < SDF_DISPATCH_AUTO || p.dispatch > SDF_DISPATCH_UNCULLED)
     return SDF_E_INVALID_ARG;
   if (sdf_format_bytes(p.output_format) < 0) return SDF_E_INVALID_ARG;
-  if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > 64)) return SDF_E_INVALID_ARG;
+  if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > sdf::kMaxAoTaps))
+    return SDF_E_INVALID_ARG;
   if (count_rows(p.height, tiling ? *tiling : kWholeFrame) < 0) return SDF_E_INVALID_ARG;
   if (scene->kind == SDF_SCENE_PRIMITIVES) {
     if (scene->count < 0 || scene->count > SDF_MAX_PRIMS) return SDF_E_INVALID_ARG;
@@ -402,6 +403,14 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.ao_base = params->ao_base;
   a.ao_falloff = params->ao_falloff;
   a.ao_strength = params->ao_strength;
+  // AO tap heights, in the oracle's fp32 operation order (oracle_core.h
+  // ambient_occlusion): t = i / (taps - 1); h = base + step * t
+  for (int i = 0; i < a.ao_taps && i < sdf::kMaxAoTaps; ++i) {
+    const float t = a.ao_taps > 1 ? (float)i / (float)(a.ao_taps - 1) : 0.0f;
+    a.ao_h[i] = params->ao_base + params->ao_step * t;
+  }
+  a.inv_width = 1.0f / (float)params->width;
+  a.inv_height = 1.0f / (float)params->height;
   a.block_rows = t.block_rows;
   a.first_block = t.first_block;
   a.block_stride = t.block_stride;
