@@ -222,6 +222,28 @@ def main():
                    "ms_per_step": round(el8 / args.steps * 1e3, 4),
                    "kernel_ms": round(sum(km8) / len(km8), 4)}
 
+    # the same frames without the gather (scaling with and
+    # without it): each rank renders its blocks only, max over ranks
+    no_gather = None
+    if world > 1:
+        buf = rd.alloc(frame, t)[0]
+        for _ in range(args.warmup):
+            rd.render(frame, t, out=buf)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rd.render(frame, t, out=buf)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el_ng = float(e.item())
+        no_gather = {"value": round(W * H * args.steps / el_ng / 1e6, 3),
+                     "fps": round(args.steps / el_ng, 2),
+                     "ms_per_step": round(el_ng / args.steps * 1e3, 4)}
+        del buf
+
     verified = None
     if world > 1 and not args.no_verify and rank == 0:
         # outside the timed region: the assembled frame of the last step must
@@ -255,6 +277,7 @@ def main():
             "fps": round(args.steps / elapsed, 2),
             "frame_verified": verified,
             "display_rgba8": display,
+            "no_gather": no_gather,
             "kernel_ms": round(kavg_ms, 4),
         }
         if flops is not None:

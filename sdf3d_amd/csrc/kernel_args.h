@@ -48,8 +48,8 @@ struct KernelArgs {
   // culling bounds (fixed-scene kernels): per primitive {centre.xyz, K} with
   // K = k + R + margin, R the radius of a sphere containing the primitive;
   // and the same for the cluster of primitives [cluster_first, count)
-  float bound[SDF_MAX_PRIMS][4];
-  float cluster[4];
+  alignas(16) float bound[SDF_MAX_PRIMS][4];   // 16-B aligned: read as float4 vector loads
+  alignas(16) float cluster[4];
   int32_t cluster_first;
   // outputs
   void* rgba;           // rows * width pixels of `format`, packed rows
