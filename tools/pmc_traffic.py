@@ -38,6 +38,10 @@ PASSES = [
      "SQ_WAIT_ANY"],
     ["SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS", "SQ_INSTS_VALU_TRANS_F32",
      "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32"],
+    ["SQ_INSTS", "SQ_INSTS_BRANCH", "SQ_IFETCH", "SQ_INST_CYCLES_SALU", "SQ_ACTIVE_INST_SCA",
+     "SQ_ACTIVE_INST_MISC"],
+    ["SQ_LEVEL_WAVES", "SQ_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_INSTS_VSKIPPED",
+     "SQ_ACTIVE_INST_VMEM", "SQ_INST_LEVEL_SMEM"],
 ]
 
 
@@ -45,7 +49,7 @@ def run_pass(counters, cfg, prec, outdir, steps):
     d = outdir / ("pmc_" + "_".join(c.lower() for c in counters)[:60])
     cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", cfg, "--precision", prec,
-           "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline"]
+           "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-display"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
     files = list(d.rglob("*counter_collection*.csv"))
     if r.returncode != 0 or not files:
