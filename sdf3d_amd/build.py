@@ -29,8 +29,11 @@ ARCH = os.environ.get("SDF3D_ARCH", "gfx950")
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-Wall", f"--offload-arch={ARCH}"]
 UNITS = [
-    ("render_exact.hip", ["-ffp-contract=off"]),
-    ("render_fast.hip", ["-ffp-contract=fast"]),
+    # -fno-slp-vectorize: on gfx950 v_pk_*_f32 issue at twice the cycles of
+    # their scalar forms (tools/valu_rates.hip) and cannot take abs modifiers,
+    # so SLP packing only adds shuffles and v_and masks (and SGPRs)
+    ("render_exact.hip", ["-ffp-contract=off", "-fno-slp-vectorize"]),
+    ("render_fast.hip", ["-ffp-contract=fast", "-fno-slp-vectorize"]),
     ("deinterleave.hip", []),
     ("heatmap.hip", []),
     ("sdf_abi.cpp", ["-ffp-contract=off", "-x", "hip"]),
