@@ -79,6 +79,30 @@ def build_library(force: bool = False, verbose: bool = True) -> Path:
     return LIB
 
 
+STATS_LIB = LIB_DIR / "libsdf3d_stats.so"
+
+
+def build_stats_library(force: bool = False, verbose: bool = True) -> Path:
+    """Debug variant of the library whose fast-precision kernel counts
+    wave-level culling / evaluation events (render_kernel.inc SDF_STATS;
+    read with sdf_debug_stats, tools/kernel_stats.py).  Not used by the
+    product path."""
+    hipcc = _hipcc()
+    odir = OBJ / "stats"
+    odir.mkdir(parents=True, exist_ok=True)
+    objs = []
+    for src, extra in UNITS:
+        s = CSRC / src
+        o = odir / (s.stem + ".o")
+        objs.append(o)
+        flags = [*extra, "-DSDF_STATS=1"] if src == "render_fast.hip" else extra
+        if force or _stale(o, [s, *HEADERS, Path(__file__)]):
+            _run([hipcc, *COMMON, *flags, "-c", s, "-o", o], verbose)
+    if force or _stale(STATS_LIB, objs):
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", STATS_LIB, *objs], verbose)
+    return STATS_LIB
+
+
 BIN_DIR = PKG / "bin"
 EXAMPLE = ROOT / "examples" / "sdf_main.cpp"
 
