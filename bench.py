@@ -291,6 +291,14 @@ def main():
                                "flops_per_launch": flops,
                                "store_GBps": round(rows * W * lib_bpp(frame) / (kavg_ms * 1e-3)
                                                    / 1e9, 1)}
+            im = pmc.get("valu_issue_model")
+            if im:
+                # hardware view: the kernel's VALU issue cycles (instruction
+                # mix x measured issue cost) over its cycles, as a range
+                out["roofline"]["valu_issue_util"] = [round(x, 3) for x in im["util"]]
+            out["roofline"]["note"] = ("achieved counts every primitive at every step "
+                                       "(SURVEY 8(d) rule); exact culling skips provably "
+                                       "dead evaluations, so frac can exceed 1")
             ex = pmc.get("executed_flops_per_launch")
             if ex:
                 # culled primitives are algorithmic work the kernel provably
