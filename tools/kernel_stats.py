@@ -56,6 +56,7 @@ def main():
             "cluster_cached_skip": round(v[1], 3),
             "cluster_fresh_test": round(v[2], 3),
             "cluster_fresh_skip": round(v[3], 3),
+            "cluster_test_forgone": round(v[28], 3),
             "prim_cached_skip": [round(x, 3) for x in v[4:12]],
             "prim_fresh_test": [round(x, 3) for x in v[12:20]],
             "prim_evaluated": [round(x, 3) for x in v[20:28]],
