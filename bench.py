@@ -57,9 +57,14 @@ def parse():
     ap.add_argument("--pose", type=int, default=0)
     ap.add_argument("--format", default="rgba32f", choices=["rgba32f", "rgba16f", "rgba8"],
                     help="framebuffer format of the assembled frame")
-    ap.add_argument("--wire", default="auto", choices=["auto", "rgba", "rgb32f"],
-                    help="N>1: what ranks send; auto = rgb32f (lossless, alpha restored on "
-                         "rank 0) for rgba32f frames, else the frame format")
+    ap.add_argument("--wire", default="auto", choices=["auto", "rgba", "rgb32f", "tiles"],
+                    help="N>1: what ranks send; auto = tiles (lossless compressed RGB32F, "
+                         "decoded into the frame on rank 0) for rgba32f frames, else the "
+                         "frame format; rgb32f = uncompressed RGB, alpha restored")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="render streams / buffer sets of the frame driver (frame i on "
+                         "stream i %% streams: a frame starts while the previous one's "
+                         "slowest tiles finish); 1 serialises launches (profiling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-stride", type=int, default=4,
                     help="CPU baseline renders every k-th 8-row block of the frame")
@@ -159,11 +164,12 @@ def main():
     frame.params.output_format = abi.FORMAT_NAMES[args.format]
     wire = args.wire
     if wire == "auto":
-        wire = "rgb32f" if (world > 1 and args.format == "rgba32f") else "rgba"
-    if wire == "rgb32f":
+        wire = "tiles" if (world > 1 and args.format == "rgba32f") else "rgba"
+    if wire in ("rgb32f", "tiles"):
         if args.format != "rgba32f":
-            sys.exit("--wire rgb32f needs --format rgba32f")
-        frame.params.output_format = abi.FORMAT_RGB32F   # ranks render RGB, root expands
+            sys.exit(f"--wire {wire} needs --format rgba32f")
+        # ranks render RGB (or its TILES stream), root assembles RGBA32F
+        frame.params.output_format = abi.FORMAT_RGB32F if wire == "rgb32f" else abi.FORMAT_TILES
     W, H = frame.params.width, frame.params.height
     rd = Renderer(dev)
     t = R.tiling(rank, world, 8)
@@ -175,13 +181,21 @@ def main():
         def render_fn(out, stream):
             rd.render(fr, t, out=out, stream=stream)
 
-        def deint_fn(parts, nparts, stride, w, h, b, out, stream):
-            rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
+        if fr.params.output_format == abi.FORMAT_TILES:
+            def tiles_fn(parts, nparts, pitch, w, h, b, out, stream):
+                rd.tiles_decode(parts, nparts, pitch, w, h, b, out=out, stream=stream)
 
-        drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
-                          dist=dist if world > 1 else None,
-                          dtype=R.torch_dtype(fr.params.output_format),
-                          wire_channels=R.channels(fr.params.output_format))
+            drv = FrameDriver(W, H, rank, world, dev, render_fn, tiles_fn,
+                              dist=dist if world > 1 else None, wire="tiles",
+                              nbuf=args.streams)
+        else:
+            def deint_fn(parts, nparts, stride, w, h, b, out, stream):
+                rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
+
+            drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
+                              dist=dist if world > 1 else None, nbuf=args.streams,
+                              dtype=R.torch_dtype(fr.params.output_format),
+                              wire_channels=R.channels(fr.params.output_format))
         k = steps + warmup
         e0 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
         e1 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
@@ -220,20 +234,25 @@ def main():
         display = {"format": "rgba8", "value": round(W * H * args.steps / el8 / 1e6, 3),
                    "fps": round(args.steps / el8, 2),
                    "ms_per_step": round(el8 / args.steps * 1e3, 4),
-                   "kernel_ms": round(sum(km8) / len(km8), 4)}
+                   "render_ms_pipelined": round(sum(km8) / len(km8), 4)}
 
     # the same frames without the gather (scaling with and
     # without it): each rank renders its blocks only, max over ranks
     no_gather = None
     if world > 1:
-        buf = rd.alloc(frame, t)[0]
-        for _ in range(args.warmup):
-            rd.render(frame, t, out=buf)
-        dist.barrier()
+        # the rank's own rows as RGBA32F, frames on alternating streams as in
+        # the driver, nothing shipped
+        fp = frame.copy()
+        fp.params.output_format = abi.FORMAT_RGBA32F
+        bufs = [rd.alloc(fp, t)[0] for _ in range(3)]
+        strs = [torch.cuda.Stream(device=dev) for _ in range(3)]
+        for i in range(args.warmup):
+            rd.render(fp, t, out=bufs[i % 3], stream=strs[i % 3])
         torch.cuda.synchronize(dev)
+        dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            rd.render(frame, t, out=buf)
+        for i in range(args.steps):
+            rd.render(fp, t, out=bufs[i % 3], stream=strs[i % 3])
         torch.cuda.synchronize(dev)
         dist.barrier()
         e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -242,7 +261,7 @@ def main():
         no_gather = {"value": round(W * H * args.steps / el_ng / 1e6, 3),
                      "fps": round(args.steps / el_ng, 2),
                      "ms_per_step": round(el_ng / args.steps * 1e3, 4)}
-        del buf
+        del bufs
 
     verified = None
     if world > 1 and not args.no_verify and rank == 0:
@@ -256,7 +275,24 @@ def main():
         verified = bool(torch.equal(got.view(torch.uint8), ref.view(torch.uint8)))
         log(f"[bench] assembled frame == single-device frame: {verified}")
 
-    kavg_ms = sum(kernel_ms) / len(kernel_ms)
+    # the render kernel's own launch duration, for the roofline: the rank's
+    # rows as RGBA32F, launches serialised on one stream with events around
+    # each (in the pipelined loop above a launch's events also span time
+    # queued behind the other streams' kernels)
+    fk = frame.copy()
+    fk.params.output_format = abi.FORMAT_RGBA32F
+    kbuf = rd.alloc(fk, t)[0]
+    ks = torch.cuda.current_stream(dev)
+    rd.render(fk, t, out=kbuf, stream=ks)
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    for a, b in kev:
+        a.record(ks)
+        rd.render(fk, t, out=kbuf, stream=ks)
+        b.record(ks)
+    torch.cuda.synchronize(dev)
+    kavg_ms = sum(a.elapsed_time(b) for a, b in kev) / len(kev)
+    del kbuf
     flops = rank_flops(frame, t, args.pose)
 
     if rank == 0:

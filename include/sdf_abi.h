@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 1
+#define SDF_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -187,12 +187,39 @@ typedef struct {
  *   RGB32F   RGBA32F without the alpha channel, which the shader always
  *            writes as 1.0 (voxel_fragment.frag:210): a lossless 12-byte
  *            wire format for multi-device frames; sdf_deinterleave expands
- *            it to an RGBA32F frame with alpha = 1.                        */
+ *            it to an RGBA32F frame with alpha = 1.
+ *   TILES    RGB32F losslessly compressed for the multi-device gather (about
+ *            4.4 instead of 12 bytes per pixel on the 4K CSG scene), decoded
+ *            bit for bit by sdf_tiles_decode.  The rendered (packed) rows
+ *            are cut into 8x8 tiles, tile t = ty * ceil(width / 8) + tx
+ *            covering packed rows 8ty.. and columns 8tx..; pixel j = 8 *
+ *            row + column of a tile.  Per tile and channel: the float bits
+ *            mapped to ordered integers u (bits ^ 0x7fffffff when the sign
+ *            is set, an involution; u = 0 outside the frame), the gradient
+ *            residual u - left - up + upleft (neighbours outside the tile
+ *            are 0; mod 2^32; its inverse is the tile's 2-D prefix sum),
+ *            zigzag-coded to z, with z := 0 for pixel 0 (it travels raw) and
+ *            for pixels outside the frame, stored as bit planes.
+ *            Stream layout (little-endian; sdf_tiles_bytes() sizes the
+ *            buffer, stream plus the encoder's scratch):
+ *              u32 used             bytes of bit-plane data
+ *              u32 ntiles
+ *              u32 offset[ntiles]   tile t's planes at data + offset[t]
+ *              head = stream + align16(8 + 4 * ntiles):
+ *                u32x4 head[ntiles] {w0 | w1 << 8 | w2 << 16, first[3]}:
+ *                                   w[c] the bit length of the tile's
+ *                                   largest z, first[c] u of pixel 0
+ *              data = head + 16 * ntiles: per tile w0 + w1 + w2 u64 planes,
+ *                                   channel by channel, plane b holding
+ *                                   bit b of z_j in bit j
+ *            The meaningful prefix of a stream is data + used bytes; plane
+ *            blocks appear in tile order.                                 */
 typedef enum {
   SDF_FORMAT_RGBA32F = 0,
   SDF_FORMAT_RGBA16F = 1,
   SDF_FORMAT_RGBA8 = 2,
-  SDF_FORMAT_RGB32F = 3
+  SDF_FORMAT_RGB32F = 3,
+  SDF_FORMAT_TILES = 4
 } sdf_format;
 
 typedef enum {
@@ -236,8 +263,13 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera,
  * negative SDF_E* code. */
 int sdf_owned_rows(int32_t height, const sdf_tiling* tiling);
 
-/* Bytes per pixel of a sdf_format (16, 8, 4, 12), or a negative SDF_E* code. */
+/* Bytes per pixel of a sdf_format (16, 8, 4, 12), or a negative SDF_E* code
+ * (SDF_E_UNSUPPORTED for TILES, whose size is per stream). */
 int sdf_format_bytes(int32_t format);
+
+/* Capacity in bytes of a TILES stream of `rows` packed rows of `width`
+ * pixels (the worst case: 32-bit residuals), or a negative SDF_E* code. */
+int64_t sdf_tiles_bytes(int32_t width, int32_t rows);
 
 /* Render the rows owned by `tiling` (NULL = whole frame) into `rgba`
  * (device, owned_rows * width pixels of params->output_format, packed as
@@ -258,6 +290,16 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera,
 int sdf_deinterleave(const void* parts, int32_t nparts,
                      int32_t part_stride_rows, int32_t width, int32_t height,
                      int32_t block_rows, int32_t format, void* frame, void* stream);
+
+/* Decode `nparts` TILES streams (part r = rank r's output for tiling
+ * {block_rows, r, nparts}; nparts = 1 with block_rows = height for a whole
+ * frame), laid out back to back in `parts` with a pitch of `part_stride`
+ * bytes, into the RGBA32F frame `frame` (height * width, alpha = 1): the
+ * de-interleave of sdf_deinterleave fused with the decode.  Device pointers;
+ * asynchronous on `stream`. */
+int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
+                     int32_t width, int32_t height, int32_t block_rows, void* frame,
+                     void* stream);
 
 /* Debug view of the `steps` output of sdf_render: `count` int2 entries
  * (primary, shadow) -> colours of `format`, with which = 0 (primary), 1

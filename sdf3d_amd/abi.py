@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 1
+SDF_ABI_VERSION = 2
 SDF_MAX_PRIMS = 16
 
 # status codes
@@ -34,9 +34,11 @@ FLAG_SHADOW, FLAG_AO = 0x1, 0x2
 NORMAL_CENTRAL, NORMAL_TETRA = 0, 1
 PRECISION_EXACT, PRECISION_FAST = 0, 1
 DISPATCH_AUTO, DISPATCH_GENERIC, DISPATCH_UNCULLED = 0, 1, 2
-FORMAT_RGBA32F, FORMAT_RGBA16F, FORMAT_RGBA8, FORMAT_RGB32F = 0, 1, 2, 3
+FORMAT_RGBA32F, FORMAT_RGBA16F, FORMAT_RGBA8, FORMAT_RGB32F, FORMAT_TILES = 0, 1, 2, 3, 4
 FORMAT_NAMES = {"rgba32f": FORMAT_RGBA32F, "rgba16f": FORMAT_RGBA16F, "rgba8": FORMAT_RGBA8,
                 "rgb32f": FORMAT_RGB32F}
+# TILES (lossless compressed RGB32F, the multi-device wire) is a byte stream
+# of per-frame length, not a pixel format: see Renderer.alloc
 FORMAT_CHANNELS = {FORMAT_RGBA32F: 4, FORMAT_RGBA16F: 4, FORMAT_RGBA8: 4, FORMAT_RGB32F: 3}
 
 
@@ -103,6 +105,9 @@ SIGNATURES = {
     "sdf_deinterleave": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                    C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_format_bytes": (C.c_int, [C.c_int32]),
+    "sdf_tiles_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
+    "sdf_tiles_decode": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
+                                   C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                               C.c_void_p, C.c_void_p]),
     "sdf_strerror": (C.c_char_p, [C.c_int]),

@@ -36,6 +36,7 @@ UNITS = [
     ("render_fast.hip", ["-ffp-contract=fast", "-fno-slp-vectorize"]),
     ("deinterleave.hip", []),
     ("heatmap.hip", []),
+    ("tiles.hip", []),
     ("sdf_abi.cpp", ["-ffp-contract=off", "-x", "hip"]),
 ]
 HEADERS = [CSRC / "kernel_args.h", CSRC / "render_kernel.inc", ROOT / "include" / "sdf_abi.h"]

@@ -6,6 +6,7 @@
 // so the fields are read with scalar loads (SGPRs), never per lane.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/sdf_abi.h"
@@ -67,6 +68,31 @@ int launch_heatmap(const int32_t* steps, int count, int which, int max_steps, in
                    void* out, void* stream);
 int launch_deinterleave_rgb(const void* parts, int nparts, int part_stride_rows, int width,
                             int height, int block_rows, void* frame, void* stream);
+int launch_tiles_decode(const void* parts, int nparts, long long part_stride, int width,
+                        int height, int block_rows, void* frame, void* stream);
+
+// ---- TILES stream buffer (sdf_abi.h SDF_FORMAT_TILES) ----------------------
+// The buffer handed to sdf_render holds the stream (header, offset table,
+// per-tile heads, worst-case plane data) followed by the encoder's scratch:
+// per-block plane-byte totals of the offset scan and fixed worst-case plane
+// slots.  sdf_tiles_bytes() = end.
+constexpr int kTilePlaneBytes = 8 * 96;   // 3 channels x 32 planes
+constexpr int kScanTiles = 2048;          // tiles per block of the offset scan
+struct TilesLayout {
+  size_t table, head, data, stream_end, bsums, slots, end;
+  __host__ __device__ explicit TilesLayout(long long ntiles) {
+    const size_t n = (size_t)ntiles;
+    const size_t nb = (n + kScanTiles - 1) / kScanTiles;
+    table = 8;
+    head = (8 + 4 * n + 15) & ~(size_t)15;
+    data = head + 16 * n;
+    stream_end = data + n * kTilePlaneBytes;
+    bsums = (stream_end + 15) & ~(size_t)15;
+    slots = (bsums + 4 * nb + 15) & ~(size_t)15;
+    end = slots + n * kTilePlaneBytes;
+  }
+};
+int launch_tiles_compact(void* stream_buf, int ntiles, void* stream);
 
 // ---- compile-time scene variants ------------------------------------------
 // A variant fixes the (kind, op) sequence of the primitive list at compile

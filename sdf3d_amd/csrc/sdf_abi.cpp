@@ -309,7 +309,8 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
     return SDF_E_INVALID_ARG;
   if (p.dispatch < SDF_DISPATCH_AUTO || p.dispatch > SDF_DISPATCH_UNCULLED)
     return SDF_E_INVALID_ARG;
-  if (sdf_format_bytes(p.output_format) < 0) return SDF_E_INVALID_ARG;
+  if (p.output_format != SDF_FORMAT_TILES && sdf_format_bytes(p.output_format) < 0)
+    return SDF_E_INVALID_ARG;
   if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > sdf::kMaxAoTaps))
     return SDF_E_INVALID_ARG;
   if (count_rows(p.height, tiling ? *tiling : kWholeFrame) < 0) return SDF_E_INVALID_ARG;
@@ -349,8 +350,17 @@ int sdf_format_bytes(int32_t format) {
     case SDF_FORMAT_RGBA16F: return 8;
     case SDF_FORMAT_RGBA8: return 4;
     case SDF_FORMAT_RGB32F: return 12;
+    case SDF_FORMAT_TILES: return SDF_E_UNSUPPORTED;   // size is per stream
     default: return SDF_E_INVALID_ARG;
   }
+}
+
+// TILES buffer: the stream (header, offset table, worst-case records of 3 x
+// 32 bit planes) and the encoder's scratch (kernel_args.h TilesLayout)
+int64_t sdf_tiles_bytes(int32_t width, int32_t rows) {
+  if (width <= 0 || rows < 0) return SDF_E_INVALID_ARG;
+  const int64_t ntiles = int64_t((width + 7) / 8) * ((rows + 7) / 8);
+  return (int64_t)sdf::TilesLayout(ntiles).end;
 }
 
 int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
@@ -431,9 +441,26 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
                        scene->kind == SDF_SCENE_PRIMITIVES;
   if (params->dispatch == SDF_DISPATCH_UNCULLED) a.cluster_first = a.prim_count;
   const int variant = generic ? sdf::kVariantGeneric : sdf::select_variant(*scene);
-  const int err = params->precision == SDF_PRECISION_FAST
-                      ? sdf::launch_render_fast(a, variant, stream)
-                      : sdf::launch_render_exact(a, variant, stream);
+  int err = params->precision == SDF_PRECISION_FAST
+                ? sdf::launch_render_fast(a, variant, stream)
+                : sdf::launch_render_exact(a, variant, stream);
+  if (err == hipSuccess && params->output_format == SDF_FORMAT_TILES)
+    err = sdf::launch_tiles_compact(rgba, ((params->width + 7) / 8) * ((rows + 7) / 8), stream);
+  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+}
+
+int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride, int32_t width,
+                     int32_t height, int32_t block_rows, void* frame, void* stream) {
+  if (!parts || !frame || nparts <= 0 || width <= 0 || height <= 0 || block_rows <= 0)
+    return SDF_E_INVALID_ARG;
+  // every part's stream must fit its pitch
+  for (int r = 0; r < nparts; ++r) {
+    const sdf_tiling t = {block_rows, r, nparts, 0};
+    const int64_t n = int64_t((width + 7) / 8) * ((count_rows(height, t) + 7) / 8);
+    if ((int64_t)sdf::TilesLayout(n).stream_end > part_stride) return SDF_E_INVALID_ARG;
+  }
+  const int err = sdf::launch_tiles_decode(parts, nparts, part_stride, width, height,
+                                           block_rows, frame, stream);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 

@@ -4,17 +4,32 @@ One process per GPU (torch.distributed; "nccl" is RCCL over xGMI on ROCm).
 Rank r of N renders the 8-row blocks r, r+N, r+2N, ... of every frame
 (sdf_tiling {8, r, N}: per-rank work within 1.006x of the mean at N = 8,
 SURVEY.md 8(e), where contiguous bands are 1.75x), packed densely.  Rank 0
-gathers the N packed parts and scatters the rows into the frame
-(sdf_deinterleave).  The reference has no multi-device path at all (one GL
-context, /root/reference/Code/src/main.cpp:48,53).
+gathers the N parts and assembles the frame.  The reference has no
+multi-device path at all (one GL context, /root/reference/Code/src/main.cpp:48,53).
 
-Pipelining: two buffer sets.  The gather of frame i is asynchronous (RCCL
-runs on its own stream) and rank 0 deinterleaves it on a side stream, so
-frame i+1 renders while frame i is in flight; a buffer is reused only after
-the collective (and on rank 0 the deinterleave) that read it has finished.
+Wire formats (what crosses xGMI):
+  "raw"    the packed rows themselves (RGBA, or RGB32F with alpha restored),
+           scattered into the frame by sdf_deinterleave.
+  "tiles"  the TILES stream (include/sdf_abi.h): lossless compressed RGB32F,
+           ~4.4 instead of 12 bytes per pixel on the 4K CSG frame, written by
+           the render kernel and decoded straight into the frame rows by
+           sdf_tiles_decode.  Streams vary in length, so the ranks agree on
+           each frame's byte count (an all-reduce MAX of one integer) before
+           gathering that many bytes from every rank.
 
-The render and deinterleave steps are injected, so the same driver runs the
-HIP kernels on GPUs (bench.py) and a CPU stand-in under the gloo backend
+Pipelining: nbuf (3) buffer sets and one render stream per set, so frame
+i+1 starts while frame i's slowest tiles finish (a launch of one rank's
+share ends with its slowest 8x8 tile: ~0.11 ms for 1/8 of the 4K frame on
+one stream, ~0.05 ms per frame on alternating streams) and while frame i is
+gathered (RCCL) and assembled (a side stream on rank 0).  In "tiles" mode
+the gather of frame i is issued after frame i+1's render, once frame i's
+size is known; every collective is issued in an order that keeps the single
+RCCL stream from holding one frame's transfer behind the next one's render.
+A buffer is reused only after the collective (and on rank 0 the assembly)
+that read it has finished.
+
+The render and assembly steps are injected, so the same driver runs the HIP
+kernels on GPUs (bench.py) and CPU stand-ins under the gloo backend
 (tests/test_multigpu_cpu.py).
 """
 from __future__ import annotations
@@ -50,89 +65,191 @@ def deinterleave_index(height: int, world: int, stride: int, block_rows: int = 8
     return r * stride + pr
 
 
+def tiles_data_offset(width: int, rows: int) -> int:
+    """Offset of the plane data in a TILES stream of `rows` packed rows
+    (include/sdf_abi.h): header, offset table, 16-B heads."""
+    n = ((width + 7) // 8) * ((rows + 7) // 8)
+    return (8 + 4 * n + 15) // 16 * 16 + 16 * n
+
+
 class FrameDriver:
     def __init__(self, width: int, height: int, rank: int, world: int, device,
                  render_fn: Callable, deinterleave_fn: Callable, block_rows: int = 8,
-                 nbuf: int = 2, dist=None, dtype=None, wire_channels: int = 4):
+                 nbuf: int = 3, dist=None, dtype=None, wire_channels: int = 4,
+                 wire: str = "raw", wire_bytes: Optional[int] = None):
         import torch
         self.torch = torch
         self.W, self.H = width, height
         self.rank, self.world = rank, world
         self.B = block_rows
         self.device = device
-        self.render_fn = render_fn          # render_fn(out_rows_tensor, stream) -> None
-        self.deinterleave_fn = deinterleave_fn  # (parts, world, stride, W, H, B, out, stream)
+        self.render_fn = render_fn          # render_fn(out_buffer, stream) -> None
+        # raw: (parts, world, stride_rows, W, H, B, out, stream)
+        # tiles: (parts, world, part_stride_bytes, W, H, B, out, stream)
+        self.deinterleave_fn = deinterleave_fn
         self.dist = dist
         self.rows = owned_rows_py(height, rank, world, block_rows)
         self.stride = owned_rows_py(height, 0, world, block_rows)  # rank 0 owns the most
         self.gpu = getattr(device, "type", str(device)).startswith("cuda")
-        self.nbuf = nbuf if world > 1 else 1
-        dtype = dtype or torch.float32   # the framebuffer format on the wire
-        mk = lambda *shape: torch.empty(shape, dtype=dtype, device=device)  # noqa: E731
-        wc = wire_channels   # 3: RGB32F wire, alpha restored by the deinterleave
-        self.local = [mk(self.stride, width, wc if world > 1 else 4) for _ in range(self.nbuf)]
-        self.works = [None] * self.nbuf
+        self.nbuf = nbuf
+        self.wire = wire if world > 1 else "raw"
         self.root = rank == 0
+        self.works = [None] * nbuf
+        if self.wire == "tiles":
+            if wire_bytes is None:
+                from .renderer import tiles_bytes
+                wire_bytes = tiles_bytes(width, self.stride)
+            self.cap = wire_bytes                     # part pitch in bytes
+            self.data_off = tiles_data_offset(width, self.rows)
+            self.local = [torch.zeros((self.cap,), dtype=torch.uint8, device=device)
+                          for _ in range(nbuf)]
+            self.sizes = [torch.zeros((1,), dtype=torch.int64, device=device)
+                          for _ in range(nbuf)]
+            self.size_works = [None] * nbuf
+            self.pending = None                       # (i, b) rendered, not yet shipped
+            if self.root:
+                self.gathered = [torch.empty((world * self.cap,), dtype=torch.uint8,
+                                             device=device) for _ in range(nbuf)]
+        else:
+            dtype = dtype or torch.float32   # the framebuffer format on the wire
+            mk = lambda *shape: torch.empty(shape, dtype=dtype, device=device)  # noqa: E731
+            wc = wire_channels   # 3: RGB32F wire, alpha restored by the deinterleave
+            self.local = [mk(self.stride, width, wc if world > 1 else 4) for _ in range(nbuf)]
+            if world > 1 and self.root:
+                self.gathered = [mk(world * self.stride, width, wc) for _ in range(nbuf)]
         if world > 1 and self.root:
-            self.gathered = [mk(world * self.stride, width, wc) for _ in range(self.nbuf)]
-            self.frames = [mk(height, width, 4) for _ in range(self.nbuf)]
-            self.deint_done = [None] * self.nbuf
-        self.stream = torch.cuda.current_stream(device) if self.gpu else None
-        self.side = torch.cuda.Stream(device=device) if (self.gpu and world > 1) else None
+            self.frames = [torch.empty((height, width, 4), dtype=torch.float32 if self.wire ==
+                                       "tiles" else (dtype or torch.float32), device=device)
+                           for _ in range(nbuf)]
+            self.asm_done = [None] * nbuf
+        if self.gpu:
+            self.streams = [torch.cuda.Stream(device=device) for _ in range(nbuf)]
+            self.side = torch.cuda.Stream(device=device) if world > 1 else None
+        else:
+            self.streams = [None] * nbuf
+            self.side = None
+
+    def _ctx(self, stream):
+        import contextlib
+        return self.torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
     def step(self, i: int, ev_before=None, ev_after=None) -> None:
-        """Render frame i (and start its gather).  Optional events bracket the
-        render launch on the render stream (kernel timing)."""
-        torch = self.torch
+        """Render frame i (and ship frame i, or in "tiles" mode frame i-1).
+        Optional events bracket the render launch on its stream."""
         b = i % self.nbuf
-        if self.world > 1 and self.works[b] is not None:
-            self.works[b].wait()            # the gather of frame i - nbuf has read local[b]
+        s = self.streams[b]
+        if self.works[b] is not None:       # the gather of frame i - nbuf read local[b]
+            with self._ctx(s):
+                self.works[b].wait()
             self.works[b] = None
-            if not self.gpu and self.root:
+            if not self.gpu and self.root and self.wire == "raw":
                 self._cpu_finish(b)
-        if ev_before is not None:
-            ev_before.record(self.stream)
-        self.render_fn(self.local[b][:self.rows], self.stream)
-        if ev_after is not None:
-            ev_after.record(self.stream)
+        with self._ctx(s):
+            if ev_before is not None:
+                ev_before.record(s)
+            out = self.local[b] if self.wire == "tiles" else self.local[b][:self.rows]
+            self.render_fn(out, s)
+            if ev_after is not None:
+                ev_after.record(s)
         if self.world == 1:
             return
-        dist = self.dist
-        if self.root:
-            if self.gpu and self.deint_done[b] is not None:
-                self.stream.wait_event(self.deint_done[b])  # deinterleave i-nbuf read gathered[b]
-            glist = [self.gathered[b][r * self.stride:(r + 1) * self.stride]
-                     for r in range(self.world)]
-            self.works[b] = dist.gather(self.local[b], gather_list=glist, dst=0, async_op=True)
-            if self.gpu:
-                with torch.cuda.stream(self.side):
-                    self.works[b].wait()    # side stream waits for the collective
-                    self.deinterleave_fn(self.gathered[b], self.world, self.stride, self.W,
-                                         self.H, self.B, self.frames[b], self.side)
-                    ev = torch.cuda.Event()
-                    ev.record(self.side)
-                    self.deint_done[b] = ev
+        if self.wire == "tiles":
+            self._step_tiles(i, b, s)
         else:
-            self.works[b] = dist.gather(self.local[b], gather_list=None, dst=0, async_op=True)
+            self._step_raw(b, s)
+
+    # ---- raw rows ------------------------------------------------------------
+    def _step_raw(self, b, s):
+        torch, dist = self.torch, self.dist
+        with self._ctx(s):
+            if self.root:
+                if self.gpu and self.asm_done[b] is not None:
+                    s.wait_event(self.asm_done[b])   # assembly of i - nbuf read gathered[b]
+                glist = [self.gathered[b][r * self.stride:(r + 1) * self.stride]
+                         for r in range(self.world)]
+                self.works[b] = dist.gather(self.local[b], gather_list=glist, dst=0,
+                                            async_op=True)
+            else:
+                self.works[b] = dist.gather(self.local[b], gather_list=None, dst=0,
+                                            async_op=True)
+        if self.root and self.gpu:
+            with torch.cuda.stream(self.side):
+                self.works[b].wait()            # side stream waits for the collective
+                self.deinterleave_fn(self.gathered[b], self.world, self.stride, self.W,
+                                     self.H, self.B, self.frames[b], self.side)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                self.asm_done[b] = ev
 
     def _cpu_finish(self, b: int) -> None:
         self.deinterleave_fn(self.gathered[b], self.world, self.stride, self.W, self.H, self.B,
                              self.frames[b], None)
 
+    # ---- TILES streams -------------------------------------------------------
+    def _step_tiles(self, i, b, s):
+        import torch.distributed as tdist
+        with self._ctx(s):
+            # this rank's stream length: data offset + `used` (header word 0)
+            used = self.local[b][:8].view(self.torch.int32)[:1].to(self.torch.int64)
+            self.sizes[b].copy_(used + self.data_off)
+        if self.pending is not None:
+            self._ship(*self.pending)
+        with self._ctx(s):
+            self.size_works[b] = self.dist.all_reduce(self.sizes[b], op=tdist.ReduceOp.MAX,
+                                                      async_op=True)
+        self.pending = (i, b)
+
+    def _ship(self, i, b):
+        """Gather frame i's streams (their agreed length) and assemble on rank 0."""
+        torch, dist = self.torch, self.dist
+        s = self.streams[b]
+        with self._ctx(s):
+            self.size_works[b].wait()
+            count = int(self.sizes[b].item())       # host sync: frame i rendered everywhere
+            self.size_works[b] = None
+            if self.root:
+                if self.gpu and self.asm_done[b] is not None:
+                    s.wait_event(self.asm_done[b])   # decode of i - nbuf read gathered[b]
+                glist = [self.gathered[b][r * self.cap:r * self.cap + count]
+                         for r in range(self.world)]
+                self.works[b] = dist.gather(self.local[b][:count], gather_list=glist, dst=0,
+                                            async_op=True)
+            else:
+                self.works[b] = dist.gather(self.local[b][:count], gather_list=None, dst=0,
+                                            async_op=True)
+        if self.root:
+            if self.gpu:
+                with torch.cuda.stream(self.side):
+                    self.works[b].wait()
+                    self.deinterleave_fn(self.gathered[b], self.world, self.cap, self.W, self.H,
+                                         self.B, self.frames[b], self.side)
+                    ev = torch.cuda.Event()
+                    ev.record(self.side)
+                    self.asm_done[b] = ev
+            else:
+                self.works[b].wait()
+                self.works[b] = None
+                self.deinterleave_fn(self.gathered[b], self.world, self.cap, self.W, self.H,
+                                     self.B, self.frames[b], None)
+
     def drain(self) -> None:
+        if self.wire == "tiles" and self.pending is not None:
+            self._ship(*self.pending)
+            self.pending = None
         for b, w in enumerate(self.works):
             if w is not None:
                 w.wait()
                 self.works[b] = None
-                if not self.gpu and self.root and self.world > 1:
+                if not self.gpu and self.root and self.world > 1 and self.wire == "raw":
                     self._cpu_finish(b)
         if self.gpu:
             self.torch.cuda.synchronize(self.device)
 
     def frame(self, i: int):
-        """Rank 0's assembled frame of step i (valid after drain())."""
+        """Rank 0's assembled frame of step i (valid after drain(); the last
+        nbuf frames are kept)."""
         if self.world == 1:
-            return self.local[0][:self.H]
+            return self.local[i % self.nbuf][:self.H]
         if not self.root:
             return None
         return self.frames[i % self.nbuf]

@@ -33,7 +33,23 @@ def torch_dtype(fmt: int):
     """torch element type of a framebuffer format."""
     import torch
     return {abi.FORMAT_RGBA32F: torch.float32, abi.FORMAT_RGBA16F: torch.float16,
-            abi.FORMAT_RGBA8: torch.uint8, abi.FORMAT_RGB32F: torch.float32}[fmt]
+            abi.FORMAT_RGBA8: torch.uint8, abi.FORMAT_RGB32F: torch.float32,
+            abi.FORMAT_TILES: torch.uint8}[fmt]
+
+
+def tiles_bytes(width: int, rows: int) -> int:
+    """Capacity of a TILES stream (sdf_tiles_bytes)."""
+    n = abi.load_library().sdf_tiles_bytes(width, rows)
+    if n < 0:
+        abi.check(int(n), "sdf_tiles_bytes")
+    return int(n)
+
+
+def tiles_stream_bytes(stream) -> int:
+    """Meaningful prefix of a TILES stream on the host: table + used records."""
+    import numpy as np
+    used, n = np.frombuffer(bytes(stream[:8].cpu().numpy()), dtype=np.uint32)
+    return (8 + 4 * int(n) + 15) // 16 * 16 + 16 * int(n) + int(used)
 
 
 def channels(fmt: int) -> int:
@@ -62,8 +78,12 @@ class Renderer:
         rows = owned_rows(frame.params.height, t)
         w = frame.params.width
         fmt = frame.params.output_format
-        rgba = self.torch.empty((rows, w, channels(fmt)), dtype=torch_dtype(fmt),
-                                device=self.device)
+        if fmt == abi.FORMAT_TILES:
+            rgba = self.torch.empty((tiles_bytes(w, rows),), dtype=self.torch.uint8,
+                                    device=self.device)
+        else:
+            rgba = self.torch.empty((rows, w, channels(fmt)), dtype=torch_dtype(fmt),
+                                    device=self.device)
         st = (self.torch.empty((rows, w, 2), dtype=self.torch.int32, device=self.device)
               if steps else None)
         return rgba, st
@@ -84,12 +104,18 @@ class Renderer:
             st = None
         if isinstance(steps, torch.Tensor):
             st = steps
-        dt = torch_dtype(frame.params.output_format)
-        ch = channels(frame.params.output_format)
-        if tuple(rgba.shape) != (rows, w, ch) or rgba.dtype != dt \
-                or not rgba.is_contiguous() or rgba.device != self.device:
-            raise ValueError(f"rgba must be a contiguous {dt} ({rows}, {w}, {ch}) tensor "
-                             f"on {self.device}")
+        if frame.params.output_format == abi.FORMAT_TILES:
+            if rows and (rgba.dtype != torch.uint8 or rgba.numel() < tiles_bytes(w, rows)
+                         or not rgba.is_contiguous() or rgba.device != self.device):
+                raise ValueError(f"a TILES stream needs a contiguous uint8 tensor of "
+                                 f">= {tiles_bytes(w, rows)} bytes on {self.device}")
+        else:
+            dt = torch_dtype(frame.params.output_format)
+            ch = channels(frame.params.output_format)
+            if tuple(rgba.shape) != (rows, w, ch) or rgba.dtype != dt \
+                    or not rgba.is_contiguous() or rgba.device != self.device:
+                raise ValueError(f"rgba must be a contiguous {dt} ({rows}, {w}, {ch}) tensor "
+                                 f"on {self.device}")
         if st is not None and (tuple(st.shape) != (rows, w, 2) or st.dtype != torch.int32
                                or not st.is_contiguous()):
             raise ValueError(f"steps must be a contiguous int32 ({rows}, {w}, 2) tensor")
@@ -143,4 +169,23 @@ class Renderer:
                                            part_stride_rows, width, height, block_rows, fmt,
                                            C.c_void_p(out.data_ptr()), self._stream(stream))
         abi.check(rc, "sdf_deinterleave")
+        return out
+
+    def tiles_decode(self, parts, nparts: int, part_stride: int, width: int, height: int,
+                     block_rows: int = 8, out=None, stream=None):
+        """Decode `nparts` TILES streams (uint8, pitch `part_stride` bytes; part
+        r from tiling {block_rows, r, nparts}) into a (height, width, 4)
+        float32 frame on this device (sdf_tiles_decode)."""
+        torch = self.torch
+        if out is None:
+            out = torch.empty((height, width, 4), dtype=torch.float32, device=self.device)
+        if parts.dtype != torch.uint8 or not parts.is_contiguous() \
+                or parts.numel() < nparts * part_stride or out.dtype != torch.float32 \
+                or tuple(out.shape) != (height, width, 4) or not out.is_contiguous():
+            raise ValueError("TILES parts / RGBA32F frame of the wrong size, layout or type")
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdf_tiles_decode(C.c_void_p(parts.data_ptr()), nparts, part_stride,
+                                           width, height, block_rows,
+                                           C.c_void_p(out.data_ptr()), self._stream(stream))
+        abi.check(rc, "sdf_tiles_decode")
         return out

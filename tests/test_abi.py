@@ -114,7 +114,31 @@ def test_render_rejects_null_output():
                         C.byref(f.material), C.byref(f.params), None, None, None, None)
     assert rc == abi.SDF_E_INVALID_ARG
     assert lib.sdf_deinterleave(None, 1, 1, 1, 1, 8, 0, None, None) == abi.SDF_E_INVALID_ARG
-    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3, 4)] == [16, 8, 4, 12, abi.SDF_E_INVALID_ARG]
+    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3, 4, 5)] == \
+        [16, 8, 4, 12, abi.SDF_E_UNSUPPORTED, abi.SDF_E_INVALID_ARG]
+    assert lib.sdf_tiles_decode(None, 1, 0, 8, 8, 8, None, None) == abi.SDF_E_INVALID_ARG
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (8, 8), (37, 23), (3840, 270)])
+def test_tiles_capacity_matches_reference(wh):
+    """sdf_tiles_bytes = the worst-case TILES stream restated in
+    tests/tiles_ref.py (header, offset table, 16-B heads, 8 * 96 plane bytes
+    per tile) plus the encoder's scratch: per-2048-tile scan totals and
+    16-B aligned plane slots."""
+    import tiles_ref
+    lib = abi.load_library()
+    n = ((wh[0] + 7) // 8) * ((wh[1] + 7) // 8)
+    nb = (n + 2047) // 2048
+    bsums = (tiles_ref.capacity(*wh) + 15) // 16 * 16
+    slots = (bsums + 4 * nb + 15) // 16 * 16
+    assert lib.sdf_tiles_bytes(*wh) == slots + n * 8 * 96
+    assert lib.sdf_tiles_bytes(0, 8) == abi.SDF_E_INVALID_ARG
+
+
+def test_validate_accepts_tiles_format():
+    f = scenes.reference()
+    f.params.output_format = abi.FORMAT_TILES
+    assert _validate(f) == abi.SDF_OK
 
 
 @pytest.mark.parametrize("height", [1, 7, 8, 9, 23, 600, 1080, 2160])

@@ -303,11 +303,14 @@ def test_cpp_host_program(renderer, tmp_path, scene_name, cfg):
     assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
 
 
-def test_multirank_bench_rehearsal(renderer, tmp_path):
-    """bench.py with 2 ranks sharing this GPU (gloo backend; RCCL needs one GPU
-    per rank): the FrameDriver's GPU path -- RGB32F wire, async gather,
-    side-stream sdf_deinterleave -- assembles frames bit-identical to a
-    single-device render."""
+@pytest.mark.parametrize("nproc,wire", [(2, "auto"), (3, "auto"), (2, "rgb32f")])
+def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire):
+    """bench.py with 2-3 ranks sharing this GPU (gloo backend; RCCL needs one
+    GPU per rank): the FrameDriver's GPU path -- alternating render streams,
+    the TILES wire (auto: kernel-written compressed streams, per-frame size
+    agreement, sdf_tiles_decode on rank 0's side stream) or the RGB32F wire
+    (sdf_deinterleave) -- assembles frames bit-identical to a single-device
+    render."""
     import json
     import socket
     import subprocess
@@ -316,15 +319,17 @@ def test_multirank_bench_rehearsal(renderer, tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     root = Path(__file__).resolve().parent.parent
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), str(root / "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1", "--backend", "gloo",
-           "--config", "C3"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           str(root / "bench.py"), "--gpus", str(nproc), "--steps", "4", "--warmup", "2",
+           "--backend", "gloo", "--config", "C3", "--wire", wire, "--no-display"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2 and d["frame_verified"] is True and d["config"]["wire"] == "rgb32f"
+    assert d["n_gpus"] == nproc and d["frame_verified"] is True
+    assert d["config"]["wire"] == ("tiles" if wire == "auto" else wire)
+    assert d["no_gather"]["value"] > 0
 
 
 def turbo_ref(steps, which, max_steps):

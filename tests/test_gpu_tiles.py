@@ -1,0 +1,151 @@
+"""GPU tests of the TILES wire format (include/sdf_abi.h SDF_FORMAT_TILES).
+
+The multi-device gather ships each rank's rows as a lossless compressed
+stream written by the render kernel itself; rank 0 decodes it straight into
+the assembled RGBA32F frame.  Lossless is the whole contract, so every test is
+bit-exact: the decoded frame must equal the RGBA32F render byte for byte.
+The format is pinned against the NumPy restatement in tests/tiles_ref.py in
+both directions (GPU stream -> NumPy decoder, NumPy stream -> GPU decoder).
+"""
+import numpy as np
+import pytest
+
+import tiles_ref
+from sdf3d_amd import abi, renderer as R, scenes
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("REF", 37, 23, 0), ("C3", 64, 64, 1), ("C3", 320, 180, 2), ("C5", 96, 72, 0),
+         ("C1", 9, 200, 0), ("C2", 200, 9, 3)]
+
+
+def frame(cfg, w, h, pose, prec, fmt):
+    f = scenes.config(cfg, w, h, precision=prec, pose=pose)
+    f.params.output_format = fmt
+    return f
+
+
+def render_pair(rd, cfg, w, h, pose, prec, t=None):
+    import torch
+    ref, _ = rd.render(frame(cfg, w, h, pose, prec, abi.FORMAT_RGBA32F), t)
+    st, _ = rd.render(frame(cfg, w, h, pose, prec, abi.FORMAT_TILES), t)
+    torch.cuda.synchronize()
+    return ref, st
+
+
+def same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint32),
+                          np.ascontiguousarray(b).view(np.uint32))
+
+
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+@pytest.mark.parametrize("cfg,w,h,pose", CASES)
+def test_tiles_round_trip_bit_exact(renderer, cfg, w, h, pose, prec):
+    import torch
+    ref, st = render_pair(renderer, cfg, w, h, pose, prec)
+    out = renderer.tiles_decode(st, 1, st.numel(), w, h)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), ref.cpu().numpy())
+    n = R.tiles_stream_bytes(st)
+    assert n <= st.numel()
+
+
+@pytest.mark.parametrize("cfg,w,h,pose", CASES[:4])
+def test_gpu_stream_decodes_with_reference(renderer, cfg, w, h, pose):
+    """The stream the kernel writes is the documented layout: byte for byte
+    the NumPy encoder's stream of the same frame, and the NumPy decoder reads
+    it back to the same bits."""
+    ref, st = render_pair(renderer, cfg, w, h, pose, abi.PRECISION_FAST)
+    s = st.cpu().numpy()
+    s = s[:tiles_ref.stream_bytes(s)]
+    assert R.tiles_stream_bytes(st) == s.size
+    host = ref.cpu().numpy()
+    e = tiles_ref.encode(host)
+    n = tiles_ref.tiles_shape(w, h)[0] * tiles_ref.tiles_shape(w, h)[1]
+    table_end, head = 8 + 4 * n, tiles_ref.head_offset(n)
+    assert s.size == e.size
+    # every defined field (the alignment gap after the offset table is not)
+    assert np.array_equal(s[:table_end], e[:table_end])
+    assert np.array_equal(s[head:], e[head:])
+    assert same_bits(tiles_ref.decode(s, w, h), host)
+
+
+@pytest.mark.parametrize("cfg,w,h,pose", CASES[:4])
+def test_reference_stream_decodes_on_gpu(renderer, cfg, w, h, pose):
+    """The GPU decoder reads streams written by the NumPy encoder."""
+    import torch
+    ref, _ = render_pair(renderer, cfg, w, h, pose, abi.PRECISION_FAST)
+    host = ref.cpu().numpy()
+    s = tiles_ref.encode(host)
+    buf = torch.zeros(tiles_ref.capacity(w, h), dtype=torch.uint8, device=renderer.device)
+    buf[:s.size] = torch.from_numpy(s).to(renderer.device)
+    out = renderer.tiles_decode(buf, 1, buf.numel(), w, h)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), host)
+
+
+def test_special_values_round_trip(renderer):
+    """NaN payloads, infinities, -0 and negative values survive the reference
+    encoder -> GPU decoder path bit for bit (the ordered map is an involution
+    and the residual arithmetic is mod 2^32)."""
+    import torch
+    rng = np.random.default_rng(5)
+    w, h = 29, 17
+    a = rng.standard_normal((h, w, 4)).astype(np.float32)
+    bits = a.view(np.uint32)
+    bits.flat[::7] = 0x7FC00123
+    bits.flat[::11] = 0x80000000
+    bits.flat[::13] = 0xFF800000
+    a[..., 3] = 1.0
+    s = tiles_ref.encode(a)
+    buf = torch.zeros(tiles_ref.capacity(w, h), dtype=torch.uint8, device=renderer.device)
+    buf[:s.size] = torch.from_numpy(s).to(renderer.device)
+    out = renderer.tiles_decode(buf, 1, buf.numel(), w, h)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("h", [64, 71, 180])
+def test_multipart_decode_assembles_frame(renderer, world, h):
+    """Each rank's TILES stream of tiling {8, r, world}, decoded together,
+    is the whole-frame RGBA32F render (decode fused with the de-interleave)."""
+    import torch
+    w = 96
+    whole, _ = renderer.render(frame("C3", w, h, 1, abi.PRECISION_FAST, abi.FORMAT_RGBA32F))
+    stride = R.tiles_bytes(w, R.owned_rows(h, R.tiling(0, world, 8)))
+    parts = torch.zeros(world * stride, dtype=torch.uint8, device=renderer.device)
+    for r in range(world):
+        t = R.tiling(r, world, 8)
+        if R.owned_rows(h, t) == 0:
+            continue
+        f = frame("C3", w, h, 1, abi.PRECISION_FAST, abi.FORMAT_TILES)
+        renderer.render(f, t, out=parts[r * stride:(r + 1) * stride])
+    out = renderer.tiles_decode(parts, world, stride, w, h, 8)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), whole.cpu().numpy())
+
+
+def test_steps_unchanged_by_tiles_output(renderer):
+    import torch
+    f32 = frame("C3", 64, 40, 2, abi.PRECISION_FAST, abi.FORMAT_RGBA32F)
+    ft = frame("C3", 64, 40, 2, abi.PRECISION_FAST, abi.FORMAT_TILES)
+    _, s1 = renderer.render(f32, steps=True)
+    _, s2 = renderer.render(ft, steps=True)
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s2)
+
+
+def test_compression_on_the_bench_scene(renderer):
+    """The point of the format: the 4K CSG frame (C4, here one 8-row band in
+    eight) ships in well under half the bytes of RGB32F."""
+    import torch
+    w, h = 3840, 2160
+    t = R.tiling(3, 8, 8)
+    f = frame("C4", w, h, 0, abi.PRECISION_FAST, abi.FORMAT_TILES)
+    st, _ = renderer.render(f, t)
+    torch.cuda.synchronize()
+    px = R.owned_rows(h, t) * w
+    bpp = R.tiles_stream_bytes(st) / px
+    print("C4 TILES bytes/pixel", round(bpp, 3))
+    assert bpp < 6.0

@@ -12,6 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
+import tiles_ref
 from sdf3d_amd import renderer as R, scenes
 from sdf3d_amd.multigpu import (FrameDriver, deinterleave_index, deinterleave_torch,
                                 owned_row_ids, owned_rows_py)
@@ -27,21 +28,45 @@ def frame_for(step):
     return scenes.config("C3", 72, 43, pose=step % 4)
 
 
+def tiles_decode_cpu(parts, world, cap, W, H, B, out, stream=None):
+    """CPU stand-in for sdf_tiles_decode: decode every rank's stream with the
+    NumPy reference and put its rows in place."""
+    p = parts.numpy()
+    for r in range(world):
+        rows = owned_rows_py(H, r, world, B)
+        if rows == 0:
+            continue
+        part = tiles_ref.decode(p[r * cap:(r + 1) * cap], W, rows)
+        out[torch.as_tensor(owned_row_ids(H, r, world, B))] = torch.from_numpy(part)
+    return out
+
+
 def _worker(rank, world, port, q, wire_channels=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         step_box = [0]
+        tiles = wire_channels == "tiles"
 
         def render_fn(out, stream):
             f = frame_for(step_box[0])
             rgba, _ = oracle.render(f, R.tiling(rank, world, 8), nthreads=1)
-            out.copy_(torch.from_numpy(rgba[..., :out.shape[-1]].copy()))
+            if tiles:
+                st = tiles_ref.encode(rgba)
+                out[:st.size] = torch.from_numpy(st)
+            else:
+                out.copy_(torch.from_numpy(rgba[..., :out.shape[-1]].copy()))
 
         f0 = frame_for(0)
-        drv = FrameDriver(f0.params.width, f0.params.height, rank, world, torch.device("cpu"),
-                          render_fn, deinterleave_torch, dist=dist,
-                          wire_channels=wire_channels)
+        W, H = f0.params.width, f0.params.height
+        if tiles:
+            drv = FrameDriver(W, H, rank, world, torch.device("cpu"), render_fn,
+                              tiles_decode_cpu, dist=dist, wire="tiles",
+                              wire_bytes=tiles_ref.capacity(W, owned_rows_py(H, 0, world)))
+        else:
+            drv = FrameDriver(W, H, rank, world, torch.device("cpu"),
+                              render_fn, deinterleave_torch, dist=dist,
+                              wire_channels=wire_channels)
         frames = []
         for i in range(5):
             step_box[0] = i
@@ -51,7 +76,7 @@ def _worker(rank, world, port, q, wire_channels=4):
         drv.drain()
         if rank == 0:
             # buffers hold the last nbuf frames
-            for i in (3, 4):
+            for i in (2, 3, 4):
                 frames.append((i, drv.frame(i).clone().numpy()))
             q.put(frames)
         dist.barrier()
@@ -59,9 +84,11 @@ def _worker(rank, world, port, q, wire_channels=4):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,wire", [(2, 4), (3, 4), (2, 3)])
+@pytest.mark.parametrize("world,wire", [(2, 4), (3, 4), (2, 3), (2, "tiles"), (3, "tiles")])
 def test_frame_driver_gloo(world, wire):
-    """wire = 3: the lossless RGB32F wire format (alpha restored on rank 0)."""
+    """wire = 3: the lossless RGB32F wire format (alpha restored on rank 0);
+    "tiles": the compressed TILES streams (NumPy codec standing in for the
+    kernels), variable-length, with the per-frame size agreement."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()

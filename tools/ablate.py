@@ -47,6 +47,8 @@ def main():
         variant("generic_culled", dispatch=abi.DISPATCH_GENERIC),
         variant("unculled", dispatch=abi.DISPATCH_UNCULLED),
         variant("max_steps_1", max_steps=1, flags=0),
+        variant("rgb32f_out", output_format=abi.FORMAT_RGB32F),
+        variant("tiles_out", output_format=abi.FORMAT_TILES),
     ]
     _ = full
     out = {v[0]: [] for v in variants}
@@ -64,6 +66,23 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             out[name].append(e0.elapsed_time(e1) / args.reps)
+    # decode of the whole-frame TILES stream into RGBA32F (rank 0's side)
+    ft = dict(variants)["tiles_out"]
+    W, H = ft.params.width, ft.params.height
+    frame = torch.empty((H, W, 4), dtype=torch.float32, device=rd.device)
+    st = bufs["tiles_out"]
+    dec = []
+    for _ in range(args.rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            rd.tiles_decode(st, 1, st.numel(), W, H, 8, out=frame)
+        e1.record()
+        torch.cuda.synchronize()
+        dec.append(e0.elapsed_time(e1) / args.reps)
+    out["tiles_decode"] = dec
+    from sdf3d_amd import renderer as R
+    out["tiles_bytes_per_px"] = [R.tiles_stream_bytes(st) / (W * H)]
     res = {k: round(statistics.median(v), 4) for k, v in out.items()}
     print(json.dumps(res, indent=1))
 

@@ -49,7 +49,8 @@ def run_pass(counters, cfg, prec, outdir, steps):
     d = outdir / ("pmc_" + "_".join(c.lower() for c in counters)[:60])
     cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", cfg, "--precision", prec,
-           "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-display"]
+           "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-display",
+           "--streams", "1"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
     files = list(d.rglob("*counter_collection*.csv"))
     if r.returncode != 0 or not files:
