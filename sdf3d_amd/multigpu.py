@@ -100,10 +100,10 @@ class FrameDriver:
                 from .renderer import tiles_bytes
                 wire_bytes = tiles_bytes(width, self.stride)
             self.cap = wire_bytes                     # part pitch in bytes
-            self.data_off = tiles_data_offset(width, self.rows)
+            # rank 0 owns the most rows, so its stream header is the longest:
+            # its data offset + the largest `used` covers every rank's stream
+            self.data_off = tiles_data_offset(width, self.stride)
             self.local = [torch.zeros((self.cap,), dtype=torch.uint8, device=device)
-                          for _ in range(nbuf)]
-            self.sizes = [torch.zeros((1,), dtype=torch.int64, device=device)
                           for _ in range(nbuf)]
             self.size_works = [None] * nbuf
             self.pending = None                       # (i, b) rendered, not yet shipped
@@ -188,16 +188,17 @@ class FrameDriver:
     # ---- TILES streams -------------------------------------------------------
     def _step_tiles(self, i, b, s):
         import torch.distributed as tdist
-        with self._ctx(s):
-            # this rank's stream length: data offset + `used` (header word 0)
-            used = self.local[b][:8].view(self.torch.int32)[:1].to(self.torch.int64)
-            self.sizes[b].copy_(used + self.data_off)
         if self.pending is not None:
             self._ship(*self.pending)
         with self._ctx(s):
-            self.size_works[b] = self.dist.all_reduce(self.sizes[b], op=tdist.ReduceOp.MAX,
+            # the ranks agree on the largest `used` (header word 0, reduced in
+            # place: the decoder reads only the offset table and the heads)
+            self.size_works[b] = self.dist.all_reduce(self._used(b), op=tdist.ReduceOp.MAX,
                                                       async_op=True)
         self.pending = (i, b)
+
+    def _used(self, b):
+        return self.local[b][:4].view(self.torch.int32)
 
     def _ship(self, i, b):
         """Gather frame i's streams (their agreed length) and assemble on rank 0."""
@@ -205,7 +206,8 @@ class FrameDriver:
         s = self.streams[b]
         with self._ctx(s):
             self.size_works[b].wait()
-            count = int(self.sizes[b].item())       # host sync: frame i rendered everywhere
+            # host sync: frame i rendered (and its size reduced) everywhere
+            count = self.data_off + int(self._used(b).item())
             self.size_works[b] = None
             if self.root:
                 if self.gpu and self.asm_done[b] is not None:
