@@ -144,15 +144,22 @@ class FrameDriver:
             self.works[b] = None
             if not self.gpu and self.root and self.wire == "raw":
                 self._cpu_finish(b)
-        with self._ctx(s):
+        out = self.local[b] if self.wire == "tiles" else self.local[b][:self.rows]
+        if self.world == 1:
+            # no collectives: the stream goes to the calls explicitly (a
+            # stream context costs more host time than a small frame renders)
             if ev_before is not None:
                 ev_before.record(s)
-            out = self.local[b] if self.wire == "tiles" else self.local[b][:self.rows]
             self.render_fn(out, s)
             if ev_after is not None:
                 ev_after.record(s)
-        if self.world == 1:
             return
+        with self._ctx(s):
+            if ev_before is not None:
+                ev_before.record(s)
+            self.render_fn(out, s)
+            if ev_after is not None:
+                ev_after.record(s)
         if self.wire == "tiles":
             self._step_tiles(i, b, s)
         else:

@@ -69,6 +69,14 @@ class Renderer:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
 
+    def _on_device(self):
+        """The HIP calls must run with this renderer's device current; enter
+        a device context only when it is not (the context costs host time)."""
+        import contextlib
+        if self.torch.cuda.current_device() == self.device.index:
+            return contextlib.nullcontext()
+        return self.torch.cuda.device(self.device)
+
     def _stream(self, stream):
         if stream is None:
             stream = self.torch.cuda.current_stream(self.device)
@@ -119,7 +127,7 @@ class Renderer:
         if st is not None and (tuple(st.shape) != (rows, w, 2) or st.dtype != torch.int32
                                or not st.is_contiguous()):
             raise ValueError(f"steps must be a contiguous int32 ({rows}, {w}, 2) tensor")
-        with torch.cuda.device(self.device):
+        with self._on_device():
             rc = self.lib.sdf_render(
                 C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
                 C.byref(frame.material), C.byref(frame.params),
@@ -183,7 +191,7 @@ class Renderer:
                 or parts.numel() < nparts * part_stride or out.dtype != torch.float32 \
                 or tuple(out.shape) != (height, width, 4) or not out.is_contiguous():
             raise ValueError("TILES parts / RGBA32F frame of the wrong size, layout or type")
-        with torch.cuda.device(self.device):
+        with self._on_device():
             rc = self.lib.sdf_tiles_decode(C.c_void_p(parts.data_ptr()), nparts, part_stride,
                                            width, height, block_rows,
                                            C.c_void_p(out.data_ptr()), self._stream(stream))
