@@ -185,9 +185,17 @@ def main():
             def tiles_fn(parts, nparts, pitch, w, h, b, out, stream):
                 rd.tiles_decode(parts, nparts, pitch, w, h, b, out=out, stream=stream)
 
+            # rank 0's own rows need no wire: rendered straight into the frame
+            froot = fr.copy()
+            froot.params.output_format = abi.FORMAT_RGBA32F
+            troot = R.tiling(rank, world, 8, frame_rows=True)
+
+            def root_fn(out, stream):
+                rd.render(froot, troot, out=out, stream=stream)
+
             drv = FrameDriver(W, H, rank, world, dev, render_fn, tiles_fn,
                               dist=dist if world > 1 else None, wire="tiles",
-                              nbuf=args.streams)
+                              nbuf=args.streams, root_render_fn=root_fn)
         else:
             def deint_fn(parts, nparts, stride, w, h, b, out, stream):
                 rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)

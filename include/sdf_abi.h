@@ -240,8 +240,14 @@ typedef struct {
   int32_t block_rows;
   int32_t first_block;
   int32_t block_stride;
-  int32_t reserved;
+  int32_t flags;      /* sdf_tiling_flags (0: packed rows) */
 } sdf_tiling;
+
+/* SDF_TILING_FRAME_ROWS: write the owned rows at their frame positions (the
+ * buffer holds `height` rows, the others untouched) instead of packed --
+ * rank 0 of a multi-device frame renders its share straight into the
+ * assembled frame.  Not with SDF_FORMAT_TILES. */
+typedef enum { SDF_TILING_FRAME_ROWS = 1 } sdf_tiling_flags;
 
 /* ---- entry points -------------------------------------------------------- */
 
@@ -295,8 +301,10 @@ int sdf_deinterleave(const void* parts, int32_t nparts,
  * {block_rows, r, nparts}; nparts = 1 with block_rows = height for a whole
  * frame), laid out back to back in `parts` with a pitch of `part_stride`
  * bytes, into the RGBA32F frame `frame` (height * width, alpha = 1): the
- * de-interleave of sdf_deinterleave fused with the decode.  Device pointers;
- * asynchronous on `stream`. */
+ * de-interleave of sdf_deinterleave fused with the decode.  A part whose
+ * header says ntiles = 0 is skipped (its rows rendered into the frame by
+ * other means, e.g. SDF_TILING_FRAME_ROWS).  Device pointers; asynchronous
+ * on `stream`. */
 int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
                      int32_t width, int32_t height, int32_t block_rows, void* frame,
                      void* stream);

@@ -35,6 +35,7 @@ NORMAL_CENTRAL, NORMAL_TETRA = 0, 1
 PRECISION_EXACT, PRECISION_FAST = 0, 1
 DISPATCH_AUTO, DISPATCH_GENERIC, DISPATCH_UNCULLED = 0, 1, 2
 FORMAT_RGBA32F, FORMAT_RGBA16F, FORMAT_RGBA8, FORMAT_RGB32F, FORMAT_TILES = 0, 1, 2, 3, 4
+TILING_FRAME_ROWS = 1
 FORMAT_NAMES = {"rgba32f": FORMAT_RGBA32F, "rgba16f": FORMAT_RGBA16F, "rgba8": FORMAT_RGBA8,
                 "rgb32f": FORMAT_RGB32F}
 # TILES (lossless compressed RGB32F, the multi-device wire) is a byte stream
@@ -83,7 +84,7 @@ class sdf_params(C.Structure):
 
 class sdf_tiling(C.Structure):
     _fields_ = [("block_rows", C.c_int32), ("first_block", C.c_int32),
-                ("block_stride", C.c_int32), ("reserved", C.c_int32)]
+                ("block_stride", C.c_int32), ("flags", C.c_int32)]
 
 
 STRUCT_SIZES = {

@@ -39,6 +39,7 @@ struct KernelArgs {
   float inv_width, inv_height;  // fast precision quad mapping
   // tiling
   int32_t block_rows, first_block, block_stride, rows;
+  int32_t frame_rows;   // SDF_TILING_FRAME_ROWS: output row = frame row y
   // scene
   int32_t scene_kind, prim_count;
   float bulb_center[3], bulb_scale, bulb_inv_scale, bulb_bail2;

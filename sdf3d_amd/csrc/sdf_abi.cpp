@@ -77,7 +77,8 @@ bool finite3(const float* v) {
 }
 
 int count_rows(int height, const sdf_tiling& t) {
-  if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0)
+  if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0 ||
+      (t.flags & ~SDF_TILING_FRAME_ROWS) != 0)
     return SDF_E_INVALID_ARG;
   const int nblocks = (height + t.block_rows - 1) / t.block_rows;
   if (t.first_block >= nblocks) return 0;
@@ -314,6 +315,8 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   if ((p.flags & SDF_FLAG_AO) && (p.ao_taps < 0 || p.ao_taps > sdf::kMaxAoTaps))
     return SDF_E_INVALID_ARG;
   if (count_rows(p.height, tiling ? *tiling : kWholeFrame) < 0) return SDF_E_INVALID_ARG;
+  if (tiling && (tiling->flags & SDF_TILING_FRAME_ROWS) && p.output_format == SDF_FORMAT_TILES)
+    return SDF_E_INVALID_ARG;   // a stream is made of packed tiles
   if (scene->kind == SDF_SCENE_PRIMITIVES) {
     if (scene->count < 0 || scene->count > SDF_MAX_PRIMS) return SDF_E_INVALID_ARG;
     for (int i = 0; i < scene->count; ++i) {
@@ -425,6 +428,7 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.first_block = t.first_block;
   a.block_stride = t.block_stride;
   a.rows = rows;
+  a.frame_rows = (t.flags & SDF_TILING_FRAME_ROWS) ? 1 : 0;
   a.scene_kind = scene->kind;
   a.prim_count = scene->kind == SDF_SCENE_PRIMITIVES ? scene->count : 0;
   for (int i = 0; i < 3; ++i) a.bulb_center[i] = scene->bulb_center[i];

@@ -78,6 +78,7 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
   const int ntiles = tiles_x * ((rows + 7) >> 3);
   if (tile >= ntiles) return;
   const uint8_t* base = parts + (long long)part * part_stride;
+  if (reinterpret_cast<const uint32_t*>(base)[1] == 0) return;   // no stream: rows rendered in place
   const TilesLayout Lt(ntiles);
   // the offset and the head depend only on the tile: both loads in flight
   const uint32_t off = reinterpret_cast<const uint32_t*>(base + Lt.table)[tile];

@@ -76,7 +76,8 @@ class FrameDriver:
     def __init__(self, width: int, height: int, rank: int, world: int, device,
                  render_fn: Callable, deinterleave_fn: Callable, block_rows: int = 8,
                  nbuf: int = 3, dist=None, dtype=None, wire_channels: int = 4,
-                 wire: str = "raw", wire_bytes: Optional[int] = None):
+                 wire: str = "raw", wire_bytes: Optional[int] = None,
+                 root_render_fn: Optional[Callable] = None):
         import torch
         self.torch = torch
         self.W, self.H = width, height
@@ -84,6 +85,10 @@ class FrameDriver:
         self.B = block_rows
         self.device = device
         self.render_fn = render_fn          # render_fn(out_buffer, stream) -> None
+        # "tiles" mode, rank 0: render its own rows straight into the frame
+        # (root_render_fn(frame, stream), SDF_TILING_FRAME_ROWS) and send an
+        # empty stream (ntiles = 0, skipped by the decode)
+        self.root_render_fn = root_render_fn if (wire == "tiles" and rank == 0) else None
         # raw: (parts, world, stride_rows, W, H, B, out, stream)
         # tiles: (parts, world, part_stride_bytes, W, H, B, out, stream)
         self.deinterleave_fn = deinterleave_fn
@@ -157,7 +162,10 @@ class FrameDriver:
         with self._ctx(s):
             if ev_before is not None:
                 ev_before.record(s)
-            self.render_fn(out, s)
+            if self.root_render_fn is not None:
+                self.root_render_fn(self.frames[b], s)
+            else:
+                self.render_fn(out, s)
             if ev_after is not None:
                 ev_after.record(s)
         if self.wire == "tiles":

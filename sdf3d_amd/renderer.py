@@ -14,12 +14,22 @@ from . import abi
 from .scenes import Frame
 
 
-def tiling(rank: int = 0, world: int = 1, block_rows: int = 8) -> abi.sdf_tiling:
+def tiling(rank: int = 0, world: int = 1, block_rows: int = 8,
+           frame_rows: bool = False) -> abi.sdf_tiling:
     """Interleaved row-block tiling: device `rank` of `world` owns blocks
-    rank, rank + world, ...."""
+    rank, rank + world, ...; frame_rows: write them at their
+    frame positions of a full-height buffer (SDF_TILING_FRAME_ROWS)."""
     t = abi.sdf_tiling()
     t.block_rows, t.first_block, t.block_stride = block_rows, rank, world
+    t.flags = abi.TILING_FRAME_ROWS if frame_rows else 0
     return t
+
+
+def buffer_rows(height: int, t: abi.sdf_tiling | None = None) -> int:
+    """Rows of the output buffer of a render with tiling `t`."""
+    if t is not None and t.flags & abi.TILING_FRAME_ROWS:
+        return height
+    return owned_rows(height, t)
 
 
 def owned_rows(height: int, t: abi.sdf_tiling | None = None) -> int:
@@ -83,7 +93,7 @@ class Renderer:
         return C.c_void_p(stream.cuda_stream)
 
     def alloc(self, frame: Frame, t: abi.sdf_tiling | None = None, steps: bool = False):
-        rows = owned_rows(frame.params.height, t)
+        rows = buffer_rows(frame.params.height, t)
         w = frame.params.width
         fmt = frame.params.output_format
         if fmt == abi.FORMAT_TILES:
@@ -103,7 +113,7 @@ class Renderer:
         Returns (rgba[rows, W, 4] float32, steps[rows, W, 2] int32 or None), both
         on the device, asynchronous on `stream` (default: torch's current)."""
         torch = self.torch
-        rows = owned_rows(frame.params.height, t)
+        rows = buffer_rows(frame.params.height, t)
         w = frame.params.width
         if out is None:
             rgba, st = self.alloc(frame, t, steps is True)

@@ -105,6 +105,10 @@ def test_validate_rejects_bad_tiling():
     for br, fb, bs in [(0, 0, 1), (8, -1, 1), (8, 0, 0)]:
         t = renderer.tiling(fb, bs, br) if bs else abi.sdf_tiling(br, fb, bs, 0)
         assert _validate(f, t) == abi.SDF_E_INVALID_ARG
+    assert _validate(f, abi.sdf_tiling(8, 0, 1, 2)) == abi.SDF_E_INVALID_ARG    # unknown flag
+    assert _validate(f, renderer.tiling(0, 2, 8, frame_rows=True)) == abi.SDF_OK
+    f.params.output_format = abi.FORMAT_TILES        # a stream is packed tiles
+    assert _validate(f, renderer.tiling(0, 2, 8, frame_rows=True)) == abi.SDF_E_INVALID_ARG
 
 
 def test_render_rejects_null_output():

@@ -149,3 +149,32 @@ def test_compression_on_the_bench_scene(renderer):
     bpp = R.tiles_stream_bytes(st) / px
     print("C4 TILES bytes/pixel", round(bpp, 3))
     assert bpp < 6.0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_frame_rows_tiling_assembles_in_place(renderer, world):
+    """SDF_TILING_FRAME_ROWS: every rank's rows written at their frame
+    positions of one buffer equal the whole-frame render; a TILES decode
+    skips a part whose header says ntiles = 0 (rank 0's rows rendered in
+    place, as the frame driver does)."""
+    import torch
+    w, h = 80, 71
+    f = frame("C3", w, h, 2, abi.PRECISION_FAST, abi.FORMAT_RGBA32F)
+    whole, _ = renderer.render(f)
+    out = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device=renderer.device)
+    for r in range(world):
+        renderer.render(f, R.tiling(r, world, 8, frame_rows=True), out=out)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), whole.cpu().numpy())
+    # rank 0 in place, ranks 1.. as TILES streams
+    out2 = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device=renderer.device)
+    renderer.render(f, R.tiling(0, world, 8, frame_rows=True), out=out2)
+    stride = R.tiles_bytes(w, R.owned_rows(h, R.tiling(0, world, 8)))
+    parts = torch.zeros(world * stride, dtype=torch.uint8, device=renderer.device)
+    ft = frame("C3", w, h, 2, abi.PRECISION_FAST, abi.FORMAT_TILES)
+    for r in range(1, world):
+        if R.owned_rows(h, R.tiling(r, world, 8)):
+            renderer.render(ft, R.tiling(r, world, 8), out=parts[r * stride:(r + 1) * stride])
+    renderer.tiles_decode(parts, world, stride, w, h, 8, out=out2)
+    torch.cuda.synchronize()
+    assert same_bits(out2.cpu().numpy(), whole.cpu().numpy())

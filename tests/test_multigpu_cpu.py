@@ -34,14 +34,14 @@ def tiles_decode_cpu(parts, world, cap, W, H, B, out, stream=None):
     p = parts.numpy()
     for r in range(world):
         rows = owned_rows_py(H, r, world, B)
-        if rows == 0:
-            continue
+        if rows == 0 or int(np.frombuffer(p[r * cap + 4:r * cap + 8].tobytes(), np.uint32)[0]) == 0:
+            continue   # no stream (rank 0 rendered its rows in place)
         part = tiles_ref.decode(p[r * cap:(r + 1) * cap], W, rows)
         out[torch.as_tensor(owned_row_ids(H, r, world, B))] = torch.from_numpy(part)
     return out
 
 
-def _worker(rank, world, port, q, wire_channels=4):
+def _worker(rank, world, port, q, wire_channels=4, direct=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -59,10 +59,17 @@ def _worker(rank, world, port, q, wire_channels=4):
 
         f0 = frame_for(0)
         W, H = f0.params.width, f0.params.height
+        def root_fn(frame, stream):
+            # rank 0's rows straight into the frame (SDF_TILING_FRAME_ROWS)
+            f = frame_for(step_box[0])
+            rgba, _ = oracle.render(f, R.tiling(0, world, 8), nthreads=1)
+            frame[torch.as_tensor(owned_row_ids(H, 0, world))] = torch.from_numpy(rgba)
+
         if tiles:
             drv = FrameDriver(W, H, rank, world, torch.device("cpu"), render_fn,
                               tiles_decode_cpu, dist=dist, wire="tiles",
-                              wire_bytes=tiles_ref.capacity(W, owned_rows_py(H, 0, world)))
+                              wire_bytes=tiles_ref.capacity(W, owned_rows_py(H, 0, world)),
+                              root_render_fn=root_fn if direct else None)
         else:
             drv = FrameDriver(W, H, rank, world, torch.device("cpu"),
                               render_fn, deinterleave_torch, dist=dist,
@@ -84,15 +91,17 @@ def _worker(rank, world, port, q, wire_channels=4):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,wire", [(2, 4), (3, 4), (2, 3), (2, "tiles"), (3, "tiles")])
-def test_frame_driver_gloo(world, wire):
+@pytest.mark.parametrize("world,wire,direct", [(2, 4, False), (3, 4, False), (2, 3, False),
+                                               (2, "tiles", False), (3, "tiles", True)])
+def test_frame_driver_gloo(world, wire, direct):
     """wire = 3: the lossless RGB32F wire format (alpha restored on rank 0);
     "tiles": the compressed TILES streams (NumPy codec standing in for the
     kernels), variable-length, with the per-frame size agreement."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire, direct))
+             for r in range(world)]
     for p in procs:
         p.start()
     frames = q.get(timeout=240)
