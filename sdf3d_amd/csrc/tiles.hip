@@ -64,50 +64,30 @@ __device__ __forceinline__ int part_rows(int height, int block_rows, int part, i
   return rows;
 }
 
-__global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ parts,
-                                                    int nparts, long long part_stride,
-                                                    int width, int height, int block_rows,
-                                                    int tiles_per_part, float4* __restrict__ frame) {
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int part = gw / tiles_per_part;
-  const int tile = gw - part * tiles_per_part;
-  if (part >= nparts) return;
-  const int rows = part_rows(height, block_rows, part, nparts);
-  const int tiles_x = (width + 7) >> 3;
-  const int ntiles = tiles_x * ((rows + 7) >> 3);
-  if (tile >= ntiles) return;
-  const uint8_t* base = parts + (long long)part * part_stride;
-  if (reinterpret_cast<const uint32_t*>(base)[1] == 0) return;   // no stream: rows rendered in place
-  const TilesLayout Lt(ntiles);
-  // the offset and the head depend only on the tile: both loads in flight
-  const uint32_t off = reinterpret_cast<const uint32_t*>(base + Lt.table)[tile];
-  const uint4 hd = reinterpret_cast<const uint4*>(base + Lt.head)[tile];
-  const uint32_t head[4] = {hd.x, hd.y, hd.z, hd.w};
-  const uint32_t widths = head[0];
+constexpr int kDecodeTiles = 8;   // tiles per wave of the decoder
+
+// one tile: planes (pa: planes 0..63, pb: 64..95) -> RGBA32F frame rows
+__device__ __forceinline__ void decode_tile(uint2 pa, uint2 pb, uint32_t widths, uint32_t f0,
+                                            uint32_t f1, uint32_t f2, int tile, int lane,
+                                            int part, int nparts, int rows, int width,
+                                            int block_rows, float4* __restrict__ frame) {
   const int nplanes = (widths & 255) + ((widths >> 8) & 255) + ((widths >> 16) & 255);
-  const uint2* planes = reinterpret_cast<const uint2*>(base + Lt.data + off);
-  // planes 0..63 (and 64..95) one per lane; transposed, lane j holds bit k
-  // of its residuals' concatenation (channel c at bits [k_c, k_c + w_c))
-  const uint2 pa = lane < nplanes ? planes[lane] : make_uint2(0u, 0u);
+  // transposed, lane j holds bit k of its residuals' concatenation (channel
+  // c at bits [k_c, k_c + w_c))
   const uint64_t ta = transpose64((uint64_t)pa.y << 32 | pa.x, lane);
-  uint64_t tb = 0;
-  if (nplanes > 64) {
-    const uint2 pb = lane + 64 < nplanes ? planes[lane + 64] : make_uint2(0u, 0u);
-    tb = transpose64((uint64_t)pb.y << 32 | pb.x, lane);
-  }
+  const uint64_t tb = nplanes > 64 ? transpose64((uint64_t)pb.y << 32 | pb.x, lane) : 0ull;
+  const uint32_t first[3] = {f0, f1, f2};
   const int col = lane & 7;
   float v[3];
   int k = 0;
 #pragma unroll
   for (int ch = 0; ch < 3; ch++) {
     const int w = (widths >> (8 * ch)) & 255;
-    // bits [k, k + w) of the 128-bit (tb:ta)
     const uint64_t lo64 = k < 64 ? (ta >> k) | (k ? tb << (64 - k) : 0ull) : tb >> (k - 64);
     uint32_t z = w ? (uint32_t)lo64 & (uint32_t)(0xFFFFFFFFull >> (32 - w)) : 0u;
     k += w;
     uint32_t r = (z >> 1) ^ (0u - (z & 1u));            // un-zigzag
-    if (lane == 0) r = head[1 + ch];                    // pixel 0 travels raw
+    if (lane == 0) r = first[ch];                       // pixel 0 travels raw
     // 2-D inclusive prefix sum over the 8x8 tile (mod 2^32)
 #pragma unroll
     for (int s = 1; s < 8; s <<= 1) {
@@ -121,6 +101,7 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
     }
     v[ch] = __uint_as_float(unordered_bits(r));
   }
+  const int tiles_x = (width + 7) >> 3;
   const int ty = tile / tiles_x;
   const int x = (tile - ty * tiles_x) * 8 + col;
   const int pr = ty * 8 + (lane >> 3);
@@ -128,6 +109,56 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
   const int blk = pr / block_rows;
   const int y = (part + blk * nparts) * block_rows + (pr - blk * block_rows);
   frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
+}
+
+// One wave = kDecodeTiles consecutive tiles of one part.  Their offsets and
+// heads arrive by one vector load each (lane i: tile i); each tile's planes
+// are loaded one tile ahead, so the load overlaps the previous tile's
+// transpose and prefix sums.
+__global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ parts,
+                                                    int nparts, long long part_stride,
+                                                    int width, int height, int block_rows,
+                                                    int waves_per_part, float4* __restrict__ frame) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int part = gw / waves_per_part;
+  if (part >= nparts) return;
+  const int tbase = (gw - part * waves_per_part) * kDecodeTiles;
+  const int rows = part_rows(height, block_rows, part, nparts);
+  const int ntiles = ((width + 7) >> 3) * ((rows + 7) >> 3);
+  if (tbase >= ntiles) return;
+  const uint8_t* base = parts + (long long)part * part_stride;
+  if (reinterpret_cast<const uint32_t*>(base)[1] == 0) return;   // no stream: rows rendered in place
+  const TilesLayout Lt(ntiles);
+  const int nt = min(kDecodeTiles, ntiles - tbase);
+  const uint32_t offv = lane < nt ? reinterpret_cast<const uint32_t*>(base + Lt.table)[tbase + lane] : 0u;
+  const uint4 hdv = lane < nt ? reinterpret_cast<const uint4*>(base + Lt.head)[tbase + lane]
+                              : make_uint4(0u, 0u, 0u, 0u);
+  const uint2* data = reinterpret_cast<const uint2*>(base + Lt.data);
+  auto planes_of = [&](int k, int np, int from) -> uint2 {
+    const uint32_t off = __builtin_amdgcn_readlane((int)offv, k);
+    return lane + from < np ? data[off / 8 + from + lane] : make_uint2(0u, 0u);
+  };
+  auto nplanes_of = [&](uint32_t w) {
+    return (int)((w & 255) + ((w >> 8) & 255) + ((w >> 16) & 255));
+  };
+  uint32_t wn = __builtin_amdgcn_readlane((int)hdv.x, 0);
+  uint2 next = planes_of(0, nplanes_of(wn), 0);
+#pragma unroll
+  for (int k = 0; k < kDecodeTiles; k++) {
+    if (k >= nt) break;
+    const uint32_t widths = wn;
+    const uint2 pa = next;
+    const int np = nplanes_of(widths);
+    const uint2 pb = np > 64 ? planes_of(k, np, 64) : make_uint2(0u, 0u);
+    if (k + 1 < nt) {                     // prefetch the next tile's planes
+      wn = __builtin_amdgcn_readlane((int)hdv.x, k + 1);
+      next = planes_of(k + 1, nplanes_of(wn), 0);
+    }
+    decode_tile(pa, pb, widths, __builtin_amdgcn_readlane((int)hdv.y, k),
+                __builtin_amdgcn_readlane((int)hdv.z, k), __builtin_amdgcn_readlane((int)hdv.w, k),
+                tbase + k, lane, part, nparts, rows, width, block_rows, frame);
+  }
 }
 
 // Offsets of the plane blocks in tile order: exclusive scan of 8 * (w0 + w1
@@ -218,11 +249,12 @@ int launch_tiles_decode(const void* parts, int nparts, long long part_stride, in
   const int nblocks = (height + block_rows - 1) / block_rows;
   const int rows0 = ((nblocks - 1) / nparts + 1) * block_rows;
   const int tiles_per_part = tiles_x * ((rows0 + 7) >> 3);
-  const long long waves = (long long)tiles_per_part * nparts;
+  const int waves_per_part = (tiles_per_part + kDecodeTiles - 1) / kDecodeTiles;
+  const long long waves = (long long)waves_per_part * nparts;
   if (waves == 0) return 0;
   hipLaunchKernelGGL(decode_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, reinterpret_cast<const uint8_t*>(parts), nparts,
-                     part_stride, width, height, block_rows, tiles_per_part,
+                     part_stride, width, height, block_rows, waves_per_part,
                      reinterpret_cast<float4*>(frame));
   return (int)hipGetLastError();
 }
