@@ -17,6 +17,10 @@ Wire formats (what crosses xGMI):
            each frame's byte count (an all-reduce MAX of one integer) before
            gathering that many bytes from every rank.
 
+Collective streams: the TILES size agreement has a process group of its
+own (its own RCCL communicator and stream) so it never queues behind a
+gather.
+
 Pipelining: nbuf (3) buffer sets and one render stream per set, so frame
 i+1 starts while frame i's slowest tiles finish (a launch of one rank's
 share ends with its slowest 8x8 tile: ~0.11 ms for 1/8 of the 4K frame on
@@ -112,6 +116,12 @@ class FrameDriver:
                           for _ in range(nbuf)]
             self.size_works = [None] * nbuf
             self.pending = None                       # (i, b) rendered, not yet shipped
+            # the size agreement runs in its own process group: its own RCCL
+            # communicator and stream, so frame i's all-reduce completes
+            # while frame i-1's gather is still on the links, and the
+            # gathers go back to back (in one group they would alternate
+            # with the all-reduces and the host's turnaround between them)
+            self.size_group = dist.new_group(ranks=list(range(world))) if dist else None
             if self.root:
                 self.gathered = [torch.empty((world * self.cap,), dtype=torch.uint8,
                                              device=device) for _ in range(nbuf)]
@@ -209,7 +219,7 @@ class FrameDriver:
             # the ranks agree on the largest `used` (header word 0, reduced in
             # place: the decoder reads only the offset table and the heads)
             self.size_works[b] = self.dist.all_reduce(self._used(b), op=tdist.ReduceOp.MAX,
-                                                      async_op=True)
+                                                      group=self.size_group, async_op=True)
         self.pending = (i, b)
 
     def _used(self, b):
