@@ -39,7 +39,13 @@
 #ifndef SDF_ABI_H
 #define SDF_ABI_H
 
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else
+/* compiled at run time by hipRTC (the library's kernel specialiser) */
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::int64_t int64_t;
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -223,7 +229,11 @@ typedef enum {
 } sdf_format;
 
 typedef enum {
-  SDF_DISPATCH_AUTO = 0,       /* specialised kernel if the scene matches one  */
+  SDF_DISPATCH_AUTO = 0,       /* specialised kernel: a built-in one when the
+                                  scene matches, else one compiled at run time
+                                  for the scene's (kind, op) sequence (hipRTC,
+                                  ~0.7 s once per sequence and process; off
+                                  with SDF3D_JIT=0), else the generic kernel  */
   SDF_DISPATCH_GENERIC = 1,    /* always the generic primitive-list kernel     */
   SDF_DISPATCH_UNCULLED = 2    /* generic kernel evaluating every primitive at
                                   every point (no bounding-volume culling): the
@@ -317,6 +327,10 @@ int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
  * pointers; asynchronous on `stream`. */
 int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_steps,
                 int32_t format, void* out, void* stream);
+
+/* Number of scene signatures compiled at run time in this process (see
+ * SDF_DISPATCH_AUTO). */
+int sdf_jit_count(void);
 
 /* Short description of a status code. */
 const char* sdf_strerror(int code);

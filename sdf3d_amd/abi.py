@@ -107,6 +107,7 @@ SIGNATURES = {
                                    C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_format_bytes": (C.c_int, [C.c_int32]),
     "sdf_tiles_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
+    "sdf_jit_count": (C.c_int, []),
     "sdf_tiles_decode": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                    C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,

@@ -6,8 +6,14 @@
 // so the fields are read with scalar loads (SGPRs), never per lane.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#else
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+#endif
 
 #include "../../include/sdf_abi.h"
 
@@ -94,6 +100,9 @@ struct TilesLayout {
   }
 };
 int launch_tiles_compact(void* stream_buf, int ntiles, void* stream);
+// run-time specialised kernel for a scene signature (jit.cpp); -1 = none
+int launch_render_jit(const KernelArgs& a, const int* sig, int n, bool exact, void* stream);
+int jit_compiled_count();
 
 // ---- compile-time scene variants ------------------------------------------
 // A variant fixes the (kind, op) sequence of the primitive list at compile
@@ -146,5 +155,6 @@ enum SceneVariant : int {
 
 // Variant for a validated scene (kVariantGeneric when no fixed one matches).
 int select_variant(const sdf_scene& scene);
+int scene_signature(const sdf_scene& scene, int* sig);
 
 }  // namespace sdf

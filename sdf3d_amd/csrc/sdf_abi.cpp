@@ -190,9 +190,9 @@ void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
 
 namespace sdf {
 
-int select_variant(const sdf_scene& scene) {
-  if (scene.kind == SDF_SCENE_MANDELBULB) return kVariantBulb;
-  int sig[SDF_MAX_PRIMS];
+// (kind, op) sequence of a primitive scene, the compile-time signature of a
+// FixedScene kernel (an upward plane through its own kind, kPrimPlaneY)
+int scene_signature(const sdf_scene& scene, int* sig) {
   const int n = scene.count;
   for (int i = 0; i < n; ++i) {
     const sdf_primitive& p = scene.prims[i];
@@ -201,6 +201,13 @@ int select_variant(const sdf_scene& scene) {
       kind = kPrimPlaneY;
     sig[i] = SDF_KO(kind, p.op);
   }
+  return n;
+}
+
+int select_variant(const sdf_scene& scene) {
+  if (scene.kind == SDF_SCENE_MANDELBULB) return kVariantBulb;
+  int sig[SDF_MAX_PRIMS];
+  const int n = scene_signature(scene, sig);
   auto match = [&](std::initializer_list<int> v) {
     if ((int)v.size() != n) return false;
     int i = 0;
@@ -445,13 +452,22 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
                        scene->kind == SDF_SCENE_PRIMITIVES;
   if (params->dispatch == SDF_DISPATCH_UNCULLED) a.cluster_first = a.prim_count;
   const int variant = generic ? sdf::kVariantGeneric : sdf::select_variant(*scene);
-  int err = params->precision == SDF_PRECISION_FAST
-                ? sdf::launch_render_fast(a, variant, stream)
-                : sdf::launch_render_exact(a, variant, stream);
+  int err = -1;
+  if (variant == sdf::kVariantGeneric && !generic && a.prim_count > 0) {
+    // no built-in specialisation: a run-time compiled one (jit.cpp)
+    int sig[SDF_MAX_PRIMS];
+    const int n = sdf::scene_signature(*scene, sig);
+    err = sdf::launch_render_jit(a, sig, n, params->precision == SDF_PRECISION_EXACT, stream);
+  }
+  if (err == -1)
+    err = params->precision == SDF_PRECISION_FAST ? sdf::launch_render_fast(a, variant, stream)
+                                                  : sdf::launch_render_exact(a, variant, stream);
   if (err == hipSuccess && params->output_format == SDF_FORMAT_TILES)
     err = sdf::launch_tiles_compact(rgba, ((params->width + 7) / 8) * ((rows + 7) / 8), stream);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
+
+int sdf_jit_count(void) { return sdf::jit_compiled_count(); }
 
 int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride, int32_t width,
                      int32_t height, int32_t block_rows, void* frame, void* stream) {

@@ -36,6 +36,13 @@ def main():
             setattr(f.params, k, v)
         return name, f
 
+    def jit_variant():
+        # the CSG8 list with its first two primitives after the plane
+        # swapped: no built-in variant matches, AUTO compiles one at run time
+        f = scenes.config(args.config, precision=abi.PRECISION_FAST)
+        f.scene.prims[1], f.scene.prims[2] = f.scene.prims[2], f.scene.prims[1]
+        return "jit_reordered", f
+
     full = abi.FLAG_SHADOW | abi.FLAG_AO
     variants = [
         variant("full"),
@@ -47,6 +54,7 @@ def main():
         variant("generic_culled", dispatch=abi.DISPATCH_GENERIC),
         variant("unculled", dispatch=abi.DISPATCH_UNCULLED),
         variant("max_steps_1", max_steps=1, flags=0),
+        jit_variant(),
         variant("rgb32f_out", output_format=abi.FORMAT_RGB32F),
         variant("tiles_out", output_format=abi.FORMAT_TILES),
     ]
