@@ -1,23 +1,26 @@
 // tiles.hip -- the TILES wire format (sdf_abi.h SDF_FORMAT_TILES) around the
 // render kernel's encoder (render_kernel.inc store_tiles):
 //
-//   compaction  the encoder leaves each tile's record in a fixed worst-case
-//               slot and its size in sizes[]; one workgroup scans the sizes
-//               into the offset table and `used`, then one wave per tile
-//               copies its record into the contiguous stream (kernel_args.h
+//   compaction  the encoder leaves each tile's planes in a fixed worst-case
+//               slot and its head (plane widths, raw first pixel) in place;
+//               tiles_scan turns the widths into block-local offsets and
+//               per-block totals, tiles_move adds the block prefix and copies
+//               each tile's planes into the contiguous stream (kernel_args.h
 //               TilesLayout).
 //   decode      fused with the multi-device de-interleave: rank r's stream
 //               holds the packed rows of tiling {block_rows, r, nparts};
-//               every record is expanded to RGBA32F (alpha 1) straight into
-//               its rows of the assembled frame.  One wave = one tile of one
-//               part (lane j = pixel 8 * row + column): the planes arrive by
-//               one vector load, each is broadcast with v_readlane, lanes
-//               gather their residual's bits, un-zigzag, and the tile's 2-D
-//               inclusive prefix sum (rows by 8-lane shuffles, then columns)
-//               inverts the gradient predictor exactly in uint32 arithmetic.
+//               every tile is expanded to RGBA32F (alpha 1) straight into its
+//               rows of the assembled frame.  Lane j = pixel (j / 8, j % 8):
+//               the planes arrive by one vector load (lane i: plane i), a
+//               64 x 64 bit transpose gives every lane the concatenation of
+//               its three residuals, then un-zigzag and the tile's 2-D
+//               inclusive prefix sum (DPP along rows, ds_bpermute along
+//               columns) invert the gradient predictor in uint32 arithmetic.
 //
-// All three are HBM-bound at a few bytes per pixel (16 out for the decode).
+// All three move a few bytes per pixel; the decode writes 16 per pixel
+// (RGBA32F) and runs ~130 VALU instructions per 8 x 8 tile.
 #include <hip/hip_runtime.h>
+
 #include <stdint.h>
 
 #include "kernel_args.h"
@@ -25,29 +28,90 @@
 namespace sdf {
 namespace {
 
-// Transpose of the 64 x 64 bit matrix whose row r is lane r's word: on
-// return lane c holds column c (bit r = bit c of lane r's input).  Six
-// butterfly stages swap the off-diagonal j x j blocks of every 2j x 2j block
-// between lanes r and r ^ j (a 64-bit shuffle, shifts, masks).
-__device__ __forceinline__ uint64_t transpose64(uint64_t a, int lane) {
-  const uint64_t masks[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+// Transpose of the 64 x 64 bit matrix whose row r is lane r's word (lo =
+// bits 0..31, hi = 32..63): on return lane c holds column c (bit r = bit c
+// of lane r's input).  Six butterfly stages exchange the off-diagonal j x j
+// blocks of every 2j x 2j block between lanes r and r ^ j:
+//   j = 32     one v_permlane32_swap (lanes 32..63 of lo <-> lanes 0..31 of hi);
+//   j <= 16    inside each 32-bit half: the partner's word (DPP quad_perm for
+//              j = 1, 2, ds_swizzle for 4, 8, 16) rotated by j toward this
+//              lane's blocks (v_alignbit, per-lane amount) and merged into
+//              them (v_bfi, per-lane mask).
+// A lane with bit j clear keeps its low blocks (mask m_j) and takes the
+// partner's low blocks shifted up by j; a lane with bit j set keeps its high
+// blocks and takes the partner's high blocks shifted down by j.
+struct TransposeLanes {
+  uint32_t keep[5], rot[5];   // stages j = 16, 8, 4, 2, 1
+  __device__ __forceinline__ explicit TransposeLanes(int lane) {
+    const uint32_t m[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
 #pragma unroll
-  for (int st = 0; st < 6; st++) {
-    const int j = 32 >> st;
-    const uint64_t m = masks[st];
-    const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)a, j);
-    const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(a >> 32), j);
-    const uint64_t p = (uint64_t)phi << 32 | plo;
-    if (lane & j) {
-      const uint64_t t = ((p >> j) ^ a) & m;        // the partner's block to take
-      a ^= t;
-    } else {
-      const uint64_t t = ((a >> j) ^ p) & m;
-      a ^= t << j;
+    for (int i = 0; i < 5; i++) {
+      const int j = 16 >> i;
+      const bool upper = lane & j;
+      keep[i] = upper ? ~m[i] : m[i];
+      rot[i] = upper ? (uint32_t)j : (uint32_t)(32 - j);   // rotate right (rotl j = rotr 32 - j)
     }
   }
-  return a;
+};
+
+template <int J>
+__device__ __forceinline__ uint32_t xor_partner(uint32_t v) {
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
+}
+
+// (a & mask) | (b & ~mask) in one v_bfi_b32 (the compiler splits it in two
+// when the mask's complement is live)
+__device__ __forceinline__ uint32_t bitfield_merge(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+  return r;
+}
+
+template <int I>
+__device__ __forceinline__ void transpose_stage(uint32_t& lo, uint32_t& hi, const TransposeLanes& T) {
+  constexpr int J = 16 >> I;
+  const uint32_t plo = xor_partner<J>(lo), phi = xor_partner<J>(hi);
+  const uint32_t qlo = __builtin_amdgcn_alignbit(plo, plo, T.rot[I]);
+  const uint32_t qhi = __builtin_amdgcn_alignbit(phi, phi, T.rot[I]);
+  lo = bitfield_merge(T.keep[I], lo, qlo);
+  hi = bitfield_merge(T.keep[I], hi, qhi);
+}
+
+__device__ __forceinline__ void transpose64(uint32_t& lo, uint32_t& hi, const TransposeLanes& T) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+  lo = sw[0];
+  hi = sw[1];
+  transpose_stage<0>(lo, hi, T);
+  transpose_stage<1>(lo, hi, T);
+  transpose_stage<2>(lo, hi, T);
+  transpose_stage<3>(lo, hi, T);
+  transpose_stage<4>(lo, hi, T);
+}
+
+// Inclusive 2-D prefix sum (mod 2^32) over the 8 x 8 tile, lane = 8 row +
+// col.  Rows: DPP row_shr by 1, 2, 4 inside the 16-lane DPP rows, the
+// sources that would cross into the next 8-lane group zeroed first (shift 4
+// masks whole banks instead).  Columns: ds_bpermute from lane - 8, - 16,
+// - 32 (addresses `up`), the wrapped-around source rows zeroed first.
+struct ScanLanes {
+  uint32_t up8, up16, up32;
+  bool c6, c5, r6, r5, r3;   // col <= 6, col <= 5, row <= 6, row <= 5, row <= 3
+  __device__ __forceinline__ explicit ScanLanes(int lane)
+      : up8(((lane - 8) & 63) << 2), up16(((lane - 16) & 63) << 2), up32(((lane - 32) & 63) << 2),
+        c6((lane & 7) <= 6), c5((lane & 7) <= 5), r6((lane >> 3) <= 6), r5((lane >> 3) <= 5),
+        r3((lane >> 3) <= 3) {}
+};
+
+__device__ __forceinline__ uint32_t scan_tile(uint32_t r, const ScanLanes& L) {
+  r += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(L.c6 ? r : 0u), 0x111, 0xF, 0xF, true);
+  r += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(L.c5 ? r : 0u), 0x112, 0xF, 0xF, true);
+  r += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x114, 0xF, 0xA, false);
+  r += (uint32_t)__builtin_amdgcn_ds_bpermute((int)L.up8, (int)(L.r6 ? r : 0u));
+  r += (uint32_t)__builtin_amdgcn_ds_bpermute((int)L.up16, (int)(L.r5 ? r : 0u));
+  r += (uint32_t)__builtin_amdgcn_ds_bpermute((int)L.up32, (int)(L.r3 ? r : 0u));
+  return r;
 }
 
 __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
@@ -64,57 +128,16 @@ __device__ __forceinline__ int part_rows(int height, int block_rows, int part, i
   return rows;
 }
 
-constexpr int kDecodeTiles = 8;   // tiles per wave of the decoder
+constexpr int kDecodeTiles = 4;   // tiles per wave of the decoder (4, 8: same speed; 16: slower)
 
-// one tile: planes (pa: planes 0..63, pb: 64..95) -> RGBA32F frame rows
-__device__ __forceinline__ void decode_tile(uint2 pa, uint2 pb, uint32_t widths, uint32_t f0,
-                                            uint32_t f1, uint32_t f2, int tile, int lane,
-                                            int part, int nparts, int rows, int width,
-                                            int block_rows, float4* __restrict__ frame) {
-  const int nplanes = (widths & 255) + ((widths >> 8) & 255) + ((widths >> 16) & 255);
-  // transposed, lane j holds bit k of its residuals' concatenation (channel
-  // c at bits [k_c, k_c + w_c))
-  const uint64_t ta = transpose64((uint64_t)pa.y << 32 | pa.x, lane);
-  const uint64_t tb = nplanes > 64 ? transpose64((uint64_t)pb.y << 32 | pb.x, lane) : 0ull;
-  const uint32_t first[3] = {f0, f1, f2};
-  const int col = lane & 7;
-  float v[3];
-  int k = 0;
-#pragma unroll
-  for (int ch = 0; ch < 3; ch++) {
-    const int w = (widths >> (8 * ch)) & 255;
-    const uint64_t lo64 = k < 64 ? (ta >> k) | (k ? tb << (64 - k) : 0ull) : tb >> (k - 64);
-    uint32_t z = w ? (uint32_t)lo64 & (uint32_t)(0xFFFFFFFFull >> (32 - w)) : 0u;
-    k += w;
-    uint32_t r = (z >> 1) ^ (0u - (z & 1u));            // un-zigzag
-    if (lane == 0) r = first[ch];                       // pixel 0 travels raw
-    // 2-D inclusive prefix sum over the 8x8 tile (mod 2^32)
-#pragma unroll
-    for (int s = 1; s < 8; s <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)r, s, 8);
-      if (col >= s) r += t;
-    }
-#pragma unroll
-    for (int s = 8; s < 64; s <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)r, s, 64);
-      if (lane >= s) r += t;
-    }
-    v[ch] = __uint_as_float(unordered_bits(r));
-  }
-  const int tiles_x = (width + 7) >> 3;
-  const int ty = tile / tiles_x;
-  const int x = (tile - ty * tiles_x) * 8 + col;
-  const int pr = ty * 8 + (lane >> 3);
-  if (x >= width || pr >= rows) return;
-  const int blk = pr / block_rows;
-  const int y = (part + blk * nparts) * block_rows + (pr - blk * block_rows);
-  frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
-}
-
-// One wave = kDecodeTiles consecutive tiles of one part.  Their offsets and
-// heads arrive by one vector load each (lane i: tile i); each tile's planes
-// are loaded one tile ahead, so the load overlaps the previous tile's
-// transpose and prefix sums.
+// One wave = TPW consecutive tiles of one part, lane j = pixel (j / 8, j % 8)
+// of each.  The memory traffic is issued up front in two dependent rounds:
+// the part header with the tiles' offsets and heads (one vector load each,
+// lane i: tile i), then every tile's first 64 planes (lane i: plane i).  Per
+// tile: transpose (lane j gets bit j of every plane: its residuals'
+// concatenation), cut out the three channels, un-zigzag, 2-D prefix sum,
+// RGBA32F store into the tile's frame rows.
+template <int TPW>
 __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ parts,
                                                     int nparts, long long part_stride,
                                                     int width, int height, int block_rows,
@@ -123,41 +146,93 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int part = gw / waves_per_part;
   if (part >= nparts) return;
-  const int tbase = (gw - part * waves_per_part) * kDecodeTiles;
+  const int tbase = (gw - part * waves_per_part) * TPW;
   const int rows = part_rows(height, block_rows, part, nparts);
-  const int ntiles = ((width + 7) >> 3) * ((rows + 7) >> 3);
+  const int tiles_x = (width + 7) >> 3;
+  const int ntiles = tiles_x * ((rows + 7) >> 3);
   if (tbase >= ntiles) return;
   const uint8_t* base = parts + (long long)part * part_stride;
-  if (reinterpret_cast<const uint32_t*>(base)[1] == 0) return;   // no stream: rows rendered in place
   const TilesLayout Lt(ntiles);
-  const int nt = min(kDecodeTiles, ntiles - tbase);
+  const int nt = min(TPW, ntiles - tbase);
+  // the header word is loaded with the tables (a part with ntiles = 0 holds
+  // no tables, but they lie inside its pitch and are discarded)
+  const uint32_t present = reinterpret_cast<const uint32_t*>(base)[1];
   const uint32_t offv = lane < nt ? reinterpret_cast<const uint32_t*>(base + Lt.table)[tbase + lane] : 0u;
   const uint4 hdv = lane < nt ? reinterpret_cast<const uint4*>(base + Lt.head)[tbase + lane]
                               : make_uint4(0u, 0u, 0u, 0u);
+  if (present == 0) return;   // no stream: rows rendered in place
   const uint2* data = reinterpret_cast<const uint2*>(base + Lt.data);
-  auto planes_of = [&](int k, int np, int from) -> uint2 {
-    const uint32_t off = __builtin_amdgcn_readlane((int)offv, k);
-    return lane + from < np ? data[off / 8 + from + lane] : make_uint2(0u, 0u);
-  };
-  auto nplanes_of = [&](uint32_t w) {
+  auto nplanes_of = [](uint32_t w) {
     return (int)((w & 255) + ((w >> 8) & 255) + ((w >> 16) & 255));
   };
-  uint32_t wn = __builtin_amdgcn_readlane((int)hdv.x, 0);
-  uint2 next = planes_of(0, nplanes_of(wn), 0);
+  uint2 pa[TPW];
 #pragma unroll
-  for (int k = 0; k < kDecodeTiles; k++) {
-    if (k >= nt) break;
-    const uint32_t widths = wn;
-    const uint2 pa = next;
-    const int np = nplanes_of(widths);
-    const uint2 pb = np > 64 ? planes_of(k, np, 64) : make_uint2(0u, 0u);
-    if (k + 1 < nt) {                     // prefetch the next tile's planes
-      wn = __builtin_amdgcn_readlane((int)hdv.x, k + 1);
-      next = planes_of(k + 1, nplanes_of(wn), 0);
+  for (int k = 0; k < TPW; k++) {
+    const int np = k < nt ? nplanes_of(__builtin_amdgcn_readlane((int)hdv.x, k)) : 0;
+    const uint32_t off = __builtin_amdgcn_readlane((int)offv, k);
+    pa[k] = lane < np ? data[off / 8 + lane] : make_uint2(0u, 0u);
+  }
+  const TransposeLanes TL(lane);
+  const ScanLanes SL(lane);
+  const int col = lane & 7, prow = lane >> 3;
+  // tile position, stepped per tile without divisions: tile column tx, tile
+  // row ty, and the block `blk` of the tiling holding packed row 8 ty at
+  // row `within` of it
+  int ty = tbase / tiles_x, tx = tbase - ty * tiles_x;
+  int blk = (8 * ty) / block_rows, within = 8 * ty - blk * block_rows;
+#pragma unroll
+  for (int k = 0; k < TPW; k++) {
+    if (k >= nt) continue;
+    if (k > 0 && ++tx == tiles_x) {
+      tx = 0;
+      ++ty;
+      within += 8;
+      while (within >= block_rows) {
+        within -= block_rows;
+        ++blk;
+      }
     }
-    decode_tile(pa, pb, widths, __builtin_amdgcn_readlane((int)hdv.y, k),
-                __builtin_amdgcn_readlane((int)hdv.z, k), __builtin_amdgcn_readlane((int)hdv.w, k),
-                tbase + k, lane, part, nparts, rows, width, block_rows, frame);
+    const uint32_t widths = __builtin_amdgcn_readlane((int)hdv.x, k);
+    const int np = nplanes_of(widths);
+    uint32_t a0 = pa[k].x, a1 = pa[k].y, b0 = 0u, b1 = 0u;   // concatenation bits 0..63, 64..95
+    transpose64(a0, a1, TL);
+    if (np > 64) {   // planes 64..95: rare (residuals wider than 21 bits on average)
+      const uint2 pb = lane + 64 < np ? data[__builtin_amdgcn_readlane((int)offv, k) / 8 + 64 + lane]
+                                      : make_uint2(0u, 0u);
+      b0 = pb.x;
+      b1 = pb.y;
+      transpose64(b0, b1, TL);
+    }
+    const uint32_t first[3] = {(uint32_t)__builtin_amdgcn_readlane((int)hdv.y, k),
+                               (uint32_t)__builtin_amdgcn_readlane((int)hdv.z, k),
+                               (uint32_t)__builtin_amdgcn_readlane((int)hdv.w, k)};
+    float v[3];
+    int kp = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+      const int w = (widths >> (8 * ch)) & 255;
+      // 32 bits of the concatenation from bit kp (kp, w wave-uniform)
+      const uint32_t x = kp < 32   ? __builtin_amdgcn_alignbit(a1, a0, kp)
+                         : kp < 64 ? __builtin_amdgcn_alignbit(b0, a1, kp - 32)
+                                   : __builtin_amdgcn_alignbit(b1, b0, kp - 64);
+      const uint32_t z = w ? x & (0xFFFFFFFFu >> (32 - w)) : 0u;
+      kp += w;
+      uint32_t r = (z >> 1) ^ (0u - (z & 1u));            // un-zigzag
+      if (lane == 0) r = first[ch];                       // pixel 0 travels raw
+      v[ch] = __uint_as_float(unordered_bits(scan_tile(r, SL)));
+    }
+    const int x = tx * 8 + col;
+    if (x < width && ty * 8 + prow < rows) {
+      // this lane's row: `prow` rows past (blk, within); a tile spans
+      // several blocks only when block_rows is not a multiple of 8
+      int b = blk, w = within + prow;
+      while (w >= block_rows) {
+        w -= block_rows;
+        ++b;
+      }
+      const int y = (part + b * nparts) * block_rows + w;
+      frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
+    }
   }
 }
 
@@ -252,7 +327,7 @@ int launch_tiles_decode(const void* parts, int nparts, long long part_stride, in
   const int waves_per_part = (tiles_per_part + kDecodeTiles - 1) / kDecodeTiles;
   const long long waves = (long long)waves_per_part * nparts;
   if (waves == 0) return 0;
-  hipLaunchKernelGGL(decode_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+  hipLaunchKernelGGL((decode_tiles<kDecodeTiles>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, reinterpret_cast<const uint8_t*>(parts), nparts,
                      part_stride, width, height, block_rows, waves_per_part,
                      reinterpret_cast<float4*>(frame));

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Rank 0's per-frame GPU work in an N-rank TILES frame, on one MI355X.
+
+At N ranks the root renders its own rows straight into the frame
+(SDF_TILING_FRAME_ROWS) on alternating streams and decodes the N - 1 peer
+streams into the same frame on a side stream; a peer renders its share as
+TILES.  Without N GPUs the peers' streams are rendered once up front and the
+root's loop is timed alone (the RCCL transfer itself is not included), so the
+frame period at N is bounded below by max(root, peer):
+
+    root_render    the root's rows only, frames on 3 streams
+    decode         the N - 1 decodes only, back to back on one stream
+    root_both      both, decode on the side stream as the frame driver does
+    root_serial    both on one stream (no overlap)
+    peer_tiles     one peer's share as TILES, frames on 3 streams
+
+    python tools/root_probe.py [--world 8] [--config C4] [--frames 200]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--only", choices=["decode", "root", "peer"], default=None,
+                    help="time one leg only (for rocprofv3 counter passes)")
+    args = ap.parse_args()
+    import torch
+    from sdf3d_amd import Renderer, abi, renderer as R, scenes
+    rd = Renderer("cuda:0")
+    N, K = args.world, args.frames
+    f = scenes.config(args.config, precision=abi.PRECISION_FAST)
+    W, H = f.params.width, f.params.height
+    ft = f.copy()
+    ft.params.output_format = abi.FORMAT_TILES
+    stride = R.tiles_bytes(W, R.owned_rows(H, R.tiling(0, N, 8)))
+    parts = torch.zeros(N * stride, dtype=torch.uint8, device=rd.device)
+    for r in range(1, N):
+        rd.render(ft, R.tiling(r, N, 8), out=parts[r * stride:(r + 1) * stride])
+    frames = [torch.empty((H, W, 4), dtype=torch.float32, device=rd.device) for _ in range(3)]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    side = torch.cuda.Stream()
+    t0_tiling = R.tiling(0, N, 8, frame_rows=True)
+    peer_bufs = [torch.empty(stride, dtype=torch.uint8, device=rd.device) for _ in range(3)]
+
+    def run(render=True, decode=True, serial=False, peer=False):
+        for b in range(3):
+            if peer:
+                rd.render(ft, R.tiling(1, N, 8), out=peer_bufs[b], stream=streams[b])
+            if render:
+                rd.render(f, t0_tiling, out=frames[b], stream=streams[b])
+            if decode:
+                rd.tiles_decode(parts, N, stride, W, H, 8, out=frames[b],
+                                stream=streams[b] if serial else side)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(K):
+            b = i % 3
+            s = streams[b]
+            if peer:
+                rd.render(ft, R.tiling(1, N, 8), out=peer_bufs[b], stream=s)
+                continue
+            if render:
+                rd.render(f, t0_tiling, out=frames[b], stream=s)
+            if decode:
+                rd.tiles_decode(parts, N, stride, W, H, 8, out=frames[b],
+                                stream=s if serial else side)
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t0) / K * 1e3, 4)
+
+    def fill():
+        for i in range(K):
+            frames[i % 3].fill_(1.0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(K):
+            frames[i % 3].fill_(1.0)
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t0) / K * 1e3, 4)
+
+    out = {"config": args.config, "world": N, "frames": K}
+    if args.only:
+        leg = {"decode": dict(render=False), "root": dict(), "peer": dict(render=False,
+               decode=False, peer=True)}[args.only]
+        out[args.only + "_ms"] = run(**leg)
+        print(json.dumps(out))
+        return
+    out["frame_fill_ms"] = fill()   # the write floor of one RGBA32F frame
+    for _ in range(2):   # second pass is the reported one
+        out["root_render_ms"] = run(decode=False)
+        out["decode_ms"] = run(render=False)
+        out["root_both_ms"] = run()
+        out["root_serial_ms"] = run(serial=True)
+        out["peer_tiles_ms"] = run(render=False, decode=False, peer=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
