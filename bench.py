@@ -61,6 +61,11 @@ def parse():
                     help="N>1: what ranks send; auto = tiles (lossless compressed RGB32F, "
                          "decoded into the frame on rank 0) for rgba32f frames, else the "
                          "frame format; rgb32f = uncompressed RGB, alpha restored")
+    ap.add_argument("--shares", default="auto",
+                    help="N>1 with the tiles wire: 'a:b' = rank 0 renders a 8-row blocks "
+                         "and every other rank b per period of a + b (N - 1) (rank 0 "
+                         "also decodes the others' streams); auto = the cost model of "
+                         "multigpu.choose_shares; other wires always 1:1")
     ap.add_argument("--streams", type=int, default=3,
                     help="render streams / buffer sets of the frame driver (frame i on "
                          "stream i %% streams: a frame starts while the previous one's "
@@ -89,9 +94,9 @@ def rank_flops(frame, tiling, pose):
     z = np.load(path)
     if int(z["width"]) != frame.params.width or int(z["height"]) != frame.params.height:
         return None
-    H, B = frame.params.height, tiling.block_rows
+    H, B, run = frame.params.height, tiling.block_rows, max(tiling.block_run, 1)
     ys = [y for y in range(H) if (y // B) >= tiling.first_block
-          and ((y // B) - tiling.first_block) % tiling.block_stride == 0]
+          and ((y // B) - tiling.first_block) % tiling.block_stride < run]
     c = costmodel.coefficients(frame)
     return c.flops(len(ys) * frame.params.width, z["row_sp"][ys].sum(), z["row_ss"][ys].sum())
 
@@ -172,30 +177,43 @@ def main():
         frame.params.output_format = abi.FORMAT_RGB32F if wire == "rgb32f" else abi.FORMAT_TILES
     W, H = frame.params.width, frame.params.height
     rd = Renderer(dev)
-    t = R.tiling(rank, world, 8)
+    # row shares: unequal only with the tiles wire (rank 0 decodes the rest)
+    shares = (1, 1)
+    if wire == "tiles" and world > 1:
+        from sdf3d_amd.multigpu import choose_shares
+        shares = (choose_shares(world) if args.shares == "auto"
+                  else tuple(int(v) for v in args.shares.split(":")))
+    t = R.tiling(rank, world, 8, shares=shares)
+    t_equal = R.tiling(rank, world, 8)
     rows = R.owned_rows(H, t)
 
     def timed_run(fr, steps, warmup):
         """warmup + `steps` timed frames of `fr` through a FrameDriver; returns
         (max-over-ranks seconds, per-launch kernel ms list, driver)."""
-        def render_fn(out, stream):
-            rd.render(fr, t, out=out, stream=stream)
+        tiles = fr.params.output_format == abi.FORMAT_TILES
+        tr = t if tiles else t_equal
 
-        if fr.params.output_format == abi.FORMAT_TILES:
-            def tiles_fn(parts, nparts, pitch, w, h, b, out, stream):
-                rd.tiles_decode(parts, nparts, pitch, w, h, b, out=out, stream=stream)
+        def render_fn(out, stream):
+            rd.render(fr, tr, out=out, stream=stream)
+
+        if tiles:
+            tilings = [R.tiling(r, world, 8, shares=shares) for r in range(world)]
+
+            def tiles_fn(parts, nparts, pitch, w, h, b, out, stream, shares=None):
+                rd.tiles_decode(parts, nparts, pitch, w, h, b, out=out, stream=stream,
+                                tilings=tilings)
 
             # rank 0's own rows need no wire: rendered straight into the frame
             froot = fr.copy()
             froot.params.output_format = abi.FORMAT_RGBA32F
-            troot = R.tiling(rank, world, 8, frame_rows=True)
+            troot = R.tiling(rank, world, 8, frame_rows=True, shares=shares)
 
             def root_fn(out, stream):
                 rd.render(froot, troot, out=out, stream=stream)
 
             drv = FrameDriver(W, H, rank, world, dev, render_fn, tiles_fn,
                               dist=dist if world > 1 else None, wire="tiles",
-                              nbuf=args.streams, root_render_fn=root_fn)
+                              nbuf=args.streams, root_render_fn=root_fn, shares=shares)
         else:
             def deint_fn(parts, nparts, stride, w, h, b, out, stream):
                 rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
@@ -315,9 +333,13 @@ def main():
                        "width": W, "height": H, "max_steps": frame.params.max_steps,
                        "precision": args.precision, "pose": args.pose,
                        "format": args.format, "wire": wire if world > 1 else None,
-                       "tiling": "8-row interleaved blocks" if world > 1 else "whole frame",
+                       "tiling": (f"8-row blocks, rank 0 {shares[0]} / others {shares[1]} per "
+                                  f"period of {shares[0] + shares[1] * (world - 1)}"
+                                  if world > 1 else "whole frame"),
                        "gather": (f"{'RCCL' if args.backend == 'nccl' else 'gloo'} gather to "
-                                  "rank 0 + sdf_deinterleave") if world > 1 else None},
+                                  "rank 0 + " + ("sdf_tiles_decode_tilings" if wire == "tiles"
+                                                 else "sdf_deinterleave"))
+                       if world > 1 else None},
             "fps": round(args.steps / elapsed, 2),
             "frame_verified": verified,
             "display_rgba8": display,

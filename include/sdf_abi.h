@@ -51,7 +51,7 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 2
+#define SDF_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -242,15 +242,21 @@ typedef enum {
 
 /* Which rows of the frame a call renders.  Rows are grouped into blocks of
  * `block_rows` rows; block b (rows [b*block_rows, (b+1)*block_rows)) is
- * rendered iff b >= first_block and (b - first_block) % block_stride == 0.
- * Rendered rows are written densely ("packed") in increasing y order, so
- * {block_rows = 8, first_block = r, block_stride = N} is device r's share
- * of an N-device interleaved tiling and {8, 0, 1} is the whole frame.        */
+ * rendered iff b >= first_block and (b - first_block) % block_stride <
+ * run, with run = max(block_run, 1) consecutive blocks per period of
+ * `block_stride` blocks.  Rendered rows are written densely ("packed") in
+ * increasing y order, so {block_rows = 8, first_block = r, block_stride = N}
+ * is device r's share of an N-device interleaved tiling and {8, 0, 1} is the
+ * whole frame; runs give devices unequal shares (the multi-device frame
+ * driver gives rank 0, which also assembles the frame, fewer rows:
+ * {8, 0, P, 0, a} for it and {8, a + b (r - 1), P, 0, b} for rank r >= 1,
+ * P = a + b (N - 1)).                                                        */
 typedef struct {
   int32_t block_rows;
   int32_t first_block;
   int32_t block_stride;
   int32_t flags;      /* sdf_tiling_flags (0: packed rows) */
+  int32_t block_run;  /* consecutive blocks per period (0 or 1: one; <= block_stride) */
 } sdf_tiling;
 
 /* SDF_TILING_FRAME_ROWS: write the owned rows at their frame positions (the
@@ -314,7 +320,15 @@ int sdf_deinterleave(const void* parts, int32_t nparts,
  * de-interleave of sdf_deinterleave fused with the decode.  A part whose
  * header says ntiles = 0 is skipped (its rows rendered into the frame by
  * other means, e.g. SDF_TILING_FRAME_ROWS).  Device pointers; asynchronous
- * on `stream`. */
+ * on `stream`.
+ * sdf_tiles_decode_tilings: part r holds the rows of tilings[r] (a host
+ * array of nparts packed tilings, at most SDF_MAX_DECODE_PARTS), e.g. the
+ * unequal shares of the frame driver; sdf_tiles_decode is the interleaved
+ * case tilings[r] = {block_rows, r, nparts, 0, 1}. */
+#define SDF_MAX_DECODE_PARTS 64
+int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_stride,
+                             const sdf_tiling* tilings, int32_t width, int32_t height,
+                             void* frame, void* stream);
 int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
                      int32_t width, int32_t height, int32_t block_rows, void* frame,
                      void* stream);

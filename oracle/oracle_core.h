@@ -325,7 +325,9 @@ static void FN(render_rows)(const sdf_scene* s, const sdf_light* li,
   (void)nthreads;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) if (nthreads > 1)
   for (int pr = 0; pr < rows; pr++) {
-    int blk = pr / t->block_rows, within = pr % t->block_rows;
+    /* period blk, row `within` of its run of blocks (sdf_abi.h sdf_tiling) */
+    int run = t->block_run > 1 ? t->block_run : 1;
+    int blk = pr / (run * t->block_rows), within = pr % (run * t->block_rows);
     int y = (t->first_block + blk * t->block_stride) * t->block_rows + within;
     (void)H;
     /* quad.y = (2y+1)/H - 1 (voxel_geometry.geom:26-52 + GL raster). */

@@ -111,10 +111,15 @@ static int make_uniforms(const sdf_camera* c, const sdf_params* p, oracle_unifor
 }
 
 static int owned_rows(int height, const sdf_tiling* t) {
-  if (t->block_rows <= 0 || t->block_stride <= 0 || t->first_block < 0) return SDF_E_INVALID_ARG;
+  int run = t->block_run > 1 ? t->block_run : 1;
+  if (t->block_rows <= 0 || t->block_stride <= 0 || t->first_block < 0 || t->block_run < 0 ||
+      run > t->block_stride)
+    return SDF_E_INVALID_ARG;
   int nblocks = (height + t->block_rows - 1) / t->block_rows;
   int rows = 0;
-  for (int b = t->first_block; b < nblocks; b += t->block_stride) {
+  /* blocks b >= first_block with (b - first_block) % block_stride < run */
+  for (int b = t->first_block; b < nblocks; b++) {
+    if ((b - t->first_block) % t->block_stride >= run) continue;
     int r = height - b * t->block_rows;
     rows += r < t->block_rows ? r : t->block_rows;
   }
@@ -191,7 +196,7 @@ static int render(int twin, const sdf_scene* s, const sdf_camera* c, const sdf_l
                   float* rgba, int* steps, int nthreads) {
   if (!s || !c || !l || !m || !p || !rgba) return SDF_E_INVALID_ARG;
   if (p->width <= 0 || p->height <= 0) return SDF_E_INVALID_ARG;
-  sdf_tiling whole = {8, 0, 1, 0};
+  sdf_tiling whole = {8, 0, 1, 0, 1};
   const sdf_tiling* t = tiling ? tiling : &whole;
   int rows = owned_rows(p->height, t);
   if (rows < 0) return rows;

@@ -10,7 +10,8 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 2
+SDF_ABI_VERSION = 3
+MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
 # status codes
@@ -84,12 +85,13 @@ class sdf_params(C.Structure):
 
 class sdf_tiling(C.Structure):
     _fields_ = [("block_rows", C.c_int32), ("first_block", C.c_int32),
-                ("block_stride", C.c_int32), ("flags", C.c_int32)]
+                ("block_stride", C.c_int32), ("flags", C.c_int32),
+                ("block_run", C.c_int32)]
 
 
 STRUCT_SIZES = {
     "sdf_primitive": 64, "sdf_scene": 8 + 64 * SDF_MAX_PRIMS + 32, "sdf_camera": 88,
-    "sdf_light": 32, "sdf_material": 40, "sdf_params": 80, "sdf_tiling": 16,
+    "sdf_light": 32, "sdf_material": 40, "sdf_params": 80, "sdf_tiling": 20,
 }
 
 # every entry point of include/sdf_abi.h: name -> (restype, argtypes)
@@ -110,6 +112,8 @@ SIGNATURES = {
     "sdf_jit_count": (C.c_int, []),
     "sdf_tiles_decode": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                    C.c_int32, C.c_void_p, C.c_void_p]),
+    "sdf_tiles_decode_tilings": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, _P(sdf_tiling),
+                                           C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                               C.c_void_p, C.c_void_p]),
     "sdf_strerror": (C.c_char_p, [C.c_int]),

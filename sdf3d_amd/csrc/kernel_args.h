@@ -45,6 +45,7 @@ struct KernelArgs {
   float inv_width, inv_height;  // fast precision quad mapping
   // tiling
   int32_t block_rows, first_block, block_stride, rows;
+  int32_t chunk_rows;   // block_rows * run: rows of one period's run of blocks
   int32_t frame_rows;   // SDF_TILING_FRAME_ROWS: output row = frame row y
   // scene
   int32_t scene_kind, prim_count;
@@ -75,8 +76,15 @@ int launch_heatmap(const int32_t* steps, int count, int which, int max_steps, in
                    void* out, void* stream);
 int launch_deinterleave_rgb(const void* parts, int nparts, int part_stride_rows, int width,
                             int height, int block_rows, void* frame, void* stream);
-int launch_tiles_decode(const void* parts, int nparts, long long part_stride, int width,
-                        int height, int block_rows, void* frame, void* stream);
+// TILES decode of parts with their own tilings (sdf_tiles_decode_tilings)
+struct DecodeParts {
+  int nparts, width, height;
+  long long part_stride;
+  int rows[SDF_MAX_DECODE_PARTS], first_block[SDF_MAX_DECODE_PARTS],
+      block_stride[SDF_MAX_DECODE_PARTS], block_rows[SDF_MAX_DECODE_PARTS],
+      chunk_rows[SDF_MAX_DECODE_PARTS];
+};
+int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, void* stream);
 
 // ---- TILES stream buffer (sdf_abi.h SDF_FORMAT_TILES) ----------------------
 // The buffer handed to sdf_render holds the stream (header, offset table,

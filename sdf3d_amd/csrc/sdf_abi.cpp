@@ -24,7 +24,7 @@ static_assert(sizeof(sdf_camera) == 88, "sdf_camera layout");
 static_assert(sizeof(sdf_light) == 32, "sdf_light layout");
 static_assert(sizeof(sdf_material) == 40, "sdf_material layout");
 static_assert(sizeof(sdf_params) == 80, "sdf_params layout");
-static_assert(sizeof(sdf_tiling) == 16, "sdf_tiling layout");
+static_assert(sizeof(sdf_tiling) == 20, "sdf_tiling layout");
 
 namespace {
 
@@ -76,20 +76,21 @@ bool finite3(const float* v) {
   return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]);
 }
 
+int run_of(const sdf_tiling& t) { return t.block_run > 1 ? t.block_run : 1; }
+
 int count_rows(int height, const sdf_tiling& t) {
   if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0 ||
-      (t.flags & ~SDF_TILING_FRAME_ROWS) != 0)
+      t.block_run < 0 || run_of(t) > t.block_stride || (t.flags & ~SDF_TILING_FRAME_ROWS) != 0)
     return SDF_E_INVALID_ARG;
-  const int nblocks = (height + t.block_rows - 1) / t.block_rows;
-  if (t.first_block >= nblocks) return 0;
-  // full blocks owned, then the (possibly partial) last block
-  const int owned = (nblocks - 1 - t.first_block) / t.block_stride + 1;
-  const int last = t.first_block + (owned - 1) * t.block_stride;
-  const int last_rows = height - last * t.block_rows;
-  return (owned - 1) * t.block_rows + (last_rows < t.block_rows ? last_rows : t.block_rows);
+  // every period contributes its run of blocks, cut at the frame's last row
+  long long rows = 0;
+  const long long B = t.block_rows;
+  for (long long b = t.first_block; b * B < height; b += t.block_stride)
+    rows += std::min<long long>((b + run_of(t)) * B, height) - b * B;
+  return (int)rows;
 }
 
-const sdf_tiling kWholeFrame = {8, 0, 1, 0};
+const sdf_tiling kWholeFrame = {8, 0, 1, 0, 1};
 
 // Per-frame preparation of the primitive parameter blocks the kernels read
 // (layouts in render_kernel.inc).  Every derived value is computed in fp32
@@ -432,6 +433,7 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
   a.inv_width = 1.0f / (float)params->width;
   a.inv_height = 1.0f / (float)params->height;
   a.block_rows = t.block_rows;
+  a.chunk_rows = t.block_rows * run_of(t);
   a.first_block = t.first_block;
   a.block_stride = t.block_stride;
   a.rows = rows;
@@ -469,19 +471,40 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
 
 int sdf_jit_count(void) { return sdf::jit_compiled_count(); }
 
+int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_stride,
+                             const sdf_tiling* tilings, int32_t width, int32_t height,
+                             void* frame, void* stream) {
+  if (!parts || !frame || !tilings || nparts <= 0 || nparts > SDF_MAX_DECODE_PARTS ||
+      width <= 0 || height <= 0)
+    return SDF_E_INVALID_ARG;
+  sdf::DecodeParts d{};
+  d.nparts = nparts;
+  d.width = width;
+  d.height = height;
+  d.part_stride = part_stride;
+  for (int r = 0; r < nparts; ++r) {
+    const sdf_tiling& t = tilings[r];
+    const int rows = count_rows(height, t);
+    if (rows < 0 || t.flags != 0) return SDF_E_INVALID_ARG;
+    // every part's stream must fit its pitch
+    const int64_t n = int64_t((width + 7) / 8) * ((rows + 7) / 8);
+    if ((int64_t)sdf::TilesLayout(n).stream_end > part_stride) return SDF_E_INVALID_ARG;
+    d.rows[r] = rows;
+    d.first_block[r] = t.first_block;
+    d.block_stride[r] = t.block_stride;
+    d.block_rows[r] = t.block_rows;
+    d.chunk_rows[r] = t.block_rows * run_of(t);
+  }
+  const int err = sdf::launch_tiles_decode(d, frame, parts, stream);
+  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+}
+
 int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride, int32_t width,
                      int32_t height, int32_t block_rows, void* frame, void* stream) {
-  if (!parts || !frame || nparts <= 0 || width <= 0 || height <= 0 || block_rows <= 0)
-    return SDF_E_INVALID_ARG;
-  // every part's stream must fit its pitch
-  for (int r = 0; r < nparts; ++r) {
-    const sdf_tiling t = {block_rows, r, nparts, 0};
-    const int64_t n = int64_t((width + 7) / 8) * ((count_rows(height, t) + 7) / 8);
-    if ((int64_t)sdf::TilesLayout(n).stream_end > part_stride) return SDF_E_INVALID_ARG;
-  }
-  const int err = sdf::launch_tiles_decode(parts, nparts, part_stride, width, height,
-                                           block_rows, frame, stream);
-  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+  if (nparts <= 0 || nparts > SDF_MAX_DECODE_PARTS || block_rows <= 0) return SDF_E_INVALID_ARG;
+  sdf_tiling t[SDF_MAX_DECODE_PARTS];
+  for (int r = 0; r < nparts; ++r) t[r] = {block_rows, r, nparts, 0, 1};
+  return sdf_tiles_decode_tilings(parts, nparts, part_stride, t, width, height, frame, stream);
 }
 
 int sdf_deinterleave(const void* parts, int32_t nparts, int32_t part_stride_rows,
@@ -493,7 +516,7 @@ int sdf_deinterleave(const void* parts, int32_t nparts, int32_t part_stride_rows
     return SDF_E_INVALID_ARG;
   // every part must hold its owned rows
   for (int r = 0; r < nparts; ++r) {
-    const sdf_tiling t = {block_rows, r, nparts, 0};
+    const sdf_tiling t = {block_rows, r, nparts, 0, 1};
     if (count_rows(height, t) > part_stride_rows) return SDF_E_INVALID_ARG;
   }
   const int err =

@@ -8,7 +8,8 @@
 //               each tile's planes into the contiguous stream (kernel_args.h
 //               TilesLayout).
 //   decode      fused with the multi-device de-interleave: rank r's stream
-//               holds the packed rows of tiling {block_rows, r, nparts};
+//               holds the packed rows of its tiling (the interleave
+//               {block_rows, r, nparts}, or any sdf_tiling per part);
 //               every tile is expanded to RGBA32F (alpha 1) straight into its
 //               rows of the assembled frame.  Lane j = pixel (j / 8, j % 8):
 //               the planes arrive by one vector load (lane i: plane i), a
@@ -118,16 +119,6 @@ __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
   return (u & 0x80000000u) ? (u ^ 0x7fffffffu) : u;
 }
 
-// rows of tiling {block_rows, part, nparts} in a frame of `height` rows
-__device__ __forceinline__ int part_rows(int height, int block_rows, int part, int nparts) {
-  const int nblocks = (height + block_rows - 1) / block_rows;
-  if (part >= nblocks) return 0;
-  const int mine = (nblocks - 1 - part) / nparts + 1;
-  int rows = mine * block_rows;
-  if ((nblocks - 1) % nparts == part) rows -= nblocks * block_rows - height;   // short last block
-  return rows;
-}
-
 constexpr int kDecodeTiles = 4;   // tiles per wave of the decoder (4, 8: same speed; 16: slower)
 
 // One wave = TPW consecutive tiles of one part, lane j = pixel (j / 8, j % 8)
@@ -138,20 +129,19 @@ constexpr int kDecodeTiles = 4;   // tiles per wave of the decoder (4, 8: same s
 // concatenation), cut out the three channels, un-zigzag, 2-D prefix sum,
 // RGBA32F store into the tile's frame rows.
 template <int TPW>
-__global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ parts,
-                                                    int nparts, long long part_stride,
-                                                    int width, int height, int block_rows,
+__global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
+                                                    const uint8_t* __restrict__ parts,
                                                     int waves_per_part, float4* __restrict__ frame) {
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int part = gw / waves_per_part;
-  if (part >= nparts) return;
+  if (part >= D.nparts) return;
   const int tbase = (gw - part * waves_per_part) * TPW;
-  const int rows = part_rows(height, block_rows, part, nparts);
+  const int rows = D.rows[part], width = D.width;
   const int tiles_x = (width + 7) >> 3;
   const int ntiles = tiles_x * ((rows + 7) >> 3);
   if (tbase >= ntiles) return;
-  const uint8_t* base = parts + (long long)part * part_stride;
+  const uint8_t* base = parts + (long long)part * D.part_stride;
   const TilesLayout Lt(ntiles);
   const int nt = min(TPW, ntiles - tbase);
   // the header word is loaded with the tables (a part with ntiles = 0 holds
@@ -176,10 +166,12 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
   const ScanLanes SL(lane);
   const int col = lane & 7, prow = lane >> 3;
   // tile position, stepped per tile without divisions: tile column tx, tile
-  // row ty, and the block `blk` of the tiling holding packed row 8 ty at
-  // row `within` of it
+  // row ty, and the period `blk` of the part's tiling holding packed row
+  // 8 ty at row `within` of its run of blocks (sdf_tiling)
+  const int chunk = D.chunk_rows[part];
+  const int first_blk = D.first_block[part], period = D.block_stride[part], brows = D.block_rows[part];
   int ty = tbase / tiles_x, tx = tbase - ty * tiles_x;
-  int blk = (8 * ty) / block_rows, within = 8 * ty - blk * block_rows;
+  int blk = (8 * ty) / chunk, within = 8 * ty - blk * chunk;
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
     if (k >= nt) continue;
@@ -187,8 +179,8 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
       tx = 0;
       ++ty;
       within += 8;
-      while (within >= block_rows) {
-        within -= block_rows;
+      while (within >= chunk) {
+        within -= chunk;
         ++blk;
       }
     }
@@ -224,13 +216,13 @@ __global__ __launch_bounds__(256) void decode_tiles(const uint8_t* __restrict__ 
     const int x = tx * 8 + col;
     if (x < width && ty * 8 + prow < rows) {
       // this lane's row: `prow` rows past (blk, within); a tile spans
-      // several blocks only when block_rows is not a multiple of 8
+      // several periods only when the run's rows are not a multiple of 8
       int b = blk, w = within + prow;
-      while (w >= block_rows) {
-        w -= block_rows;
+      while (w >= chunk) {
+        w -= chunk;
         ++b;
       }
-      const int y = (part + b * nparts) * block_rows + w;
+      const int y = (first_blk + b * period) * brows + w;
       frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
     }
   }
@@ -317,20 +309,17 @@ int launch_tiles_compact(void* stream_buf, int ntiles, void* stream) {
   return (int)hipGetLastError();
 }
 
-int launch_tiles_decode(const void* parts, int nparts, long long part_stride, int width,
-                        int height, int block_rows, void* frame, void* stream) {
-  const int tiles_x = (width + 7) >> 3;
-  // part 0 owns the most rows of an interleaved tiling
-  const int nblocks = (height + block_rows - 1) / block_rows;
-  const int rows0 = ((nblocks - 1) / nparts + 1) * block_rows;
-  const int tiles_per_part = tiles_x * ((rows0 + 7) >> 3);
+int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, void* stream) {
+  const int tiles_x = (d.width + 7) >> 3;
+  int max_rows = 0;
+  for (int r = 0; r < d.nparts; ++r) max_rows = max_rows > d.rows[r] ? max_rows : d.rows[r];
+  const int tiles_per_part = tiles_x * ((max_rows + 7) >> 3);
   const int waves_per_part = (tiles_per_part + kDecodeTiles - 1) / kDecodeTiles;
-  const long long waves = (long long)waves_per_part * nparts;
+  const long long waves = (long long)waves_per_part * d.nparts;
   if (waves == 0) return 0;
   hipLaunchKernelGGL((decode_tiles<kDecodeTiles>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, reinterpret_cast<const uint8_t*>(parts), nparts,
-                     part_stride, width, height, block_rows, waves_per_part,
-                     reinterpret_cast<float4*>(frame));
+                     (hipStream_t)stream, d, reinterpret_cast<const uint8_t*>(parts),
+                     waves_per_part, reinterpret_cast<float4*>(frame));
   return (int)hipGetLastError();
 }
 

@@ -4,7 +4,10 @@ One process per GPU (torch.distributed; "nccl" is RCCL over xGMI on ROCm).
 Rank r of N renders the 8-row blocks r, r+N, r+2N, ... of every frame
 (sdf_tiling {8, r, N}: per-rank work within 1.006x of the mean at N = 8,
 SURVEY.md 8(e), where contiguous bands are 1.75x), packed densely.  Rank 0
-gathers the N parts and assembles the frame.  The reference has no
+gathers the N parts and assembles the frame.  With the TILES wire the
+shares can be unequal (shares = (a, b): rank 0 owns a blocks and every other
+rank b per period of a + b (N - 1), choose_shares): rank 0 also decodes the
+other ranks' streams, so at N = 8 it gets 1 block in 15.  The reference has no
 multi-device path at all (one GL context, /root/reference/Code/src/main.cpp:48,53).
 
 Wire formats (what crosses xGMI):
@@ -25,7 +28,8 @@ Pipelining: nbuf (3) buffer sets and one render stream per set, so frame
 i+1 starts while frame i's slowest tiles finish (a launch of one rank's
 share ends with its slowest 8x8 tile: ~0.11 ms for 1/8 of the 4K frame on
 one stream, ~0.05 ms per frame on alternating streams) and while frame i is
-gathered (RCCL) and assembled (a side stream on rank 0).  In "tiles" mode
+gathered (RCCL) and assembled on rank 0 (TILES: on frame i's own render
+stream; raw rows: on a side stream).  In "tiles" mode
 the gather of frame i is issued after frame i+1's render, once frame i's
 size is known; every collective is issued in an order that keeps the single
 RCCL stream from holding one frame's transfer behind the next one's render.
@@ -43,20 +47,64 @@ from typing import Callable, Optional
 import numpy as np
 
 
-def owned_rows_py(height: int, rank: int, world: int, block_rows: int = 8) -> int:
-    """Rows of an interleaved tiling, in Python (mirror of sdf_owned_rows)."""
-    nblocks = (height + block_rows - 1) // block_rows
-    rows = 0
-    for b in range(rank, nblocks, world):
-        rows += min(block_rows, height - b * block_rows)
-    return rows
+def share_blocks(rank: int, world: int, shares=(1, 1)) -> tuple[int, int, int]:
+    """(first block, run, period) of `rank` in the tiling with shares (a, b):
+    per period of P = a + b (world - 1) blocks rank 0 owns the first a, rank
+    r >= 1 the b from a + b (r - 1) on (renderer.tiling, sdf_tiling)."""
+    a, b = shares
+    period = a + b * (world - 1)
+    return (0, a, period) if rank == 0 else (a + b * (rank - 1), b, period)
 
 
-def owned_row_ids(height: int, rank: int, world: int, block_rows: int = 8) -> np.ndarray:
+def owned_row_ids(height: int, rank: int, world: int, block_rows: int = 8,
+                  shares=(1, 1)) -> np.ndarray:
     """Frame rows (y) owned by `rank`, in packed order."""
+    first, run, period = share_blocks(rank, world, shares)
     y = np.arange(height)
     b = y // block_rows
-    return y[(b % world) == rank] if world > 1 else y
+    return y[(b >= first) & ((b - first) % period < run)]
+
+
+def owned_rows_py(height: int, rank: int, world: int, block_rows: int = 8,
+                  shares=(1, 1)) -> int:
+    """Rows of a rank's tiling, in Python (mirror of sdf_owned_rows)."""
+    return int(owned_row_ids(height, rank, world, block_rows, shares).size)
+
+
+# Per-frame GPU costs of the 4K CSG frame (C4) on one MI355X, in ms of one
+# whole frame (tools/root_probe.py, profiles/r01_root_probe_C4.json): the
+# rows rendered straight into the frame; the rows rendered as a TILES
+# stream (render + encoding); the TILES decode; and the floor of a small
+# share's render (its launch ends with its slowest tiles even on alternating
+# streams: 1/15 and 1/22 of the frame both take ~0.027 ms).
+FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.44, "decode": 0.040, "floor": 0.026}
+
+
+def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int]:
+    """Shares (a, b) for the TILES frame driver: rank 0 renders its rows in
+    place and decodes everyone else's, so it gets fewer rows.  Minimises the
+    larger of rank 0's per-frame work, max(a/P render, floor) + (1 - a/P)
+    decode, and a peer's, max(b/P render_tiles, floor) (P = a + b (world -
+    1)); ties go to the shorter period.  Measured at N = 8 (rank 0 / busiest
+    peer, ms per frame): 1:1 0.078 / 0.056, 1:2 0.060 / 0.059, 1:3 0.054 /
+    0.062."""
+    c = costs or FRAME_COSTS_MS
+    if world <= 1:
+        return (1, 1)
+    best = None
+    for period_first in range(2, 2 * max_blocks + 1):
+        for a in range(1, max_blocks + 1):
+            for b in range(1, max_blocks + 1):
+                if a + b != period_first:
+                    continue
+                P = a + b * (world - 1)
+                floor = c.get("floor", 0.0)
+                root = max(a / P * c["render"], floor) + (1 - a / P) * c["decode"]
+                peer = max(b / P * c["render_tiles"], floor)
+                t = max(root, peer)
+                if best is None or t < best[0] * (1 - 1e-6):
+                    best = (t, (a, b))
+    return best[1]
 
 
 def deinterleave_index(height: int, world: int, stride: int, block_rows: int = 8) -> np.ndarray:
@@ -81,7 +129,7 @@ class FrameDriver:
                  render_fn: Callable, deinterleave_fn: Callable, block_rows: int = 8,
                  nbuf: int = 3, dist=None, dtype=None, wire_channels: int = 4,
                  wire: str = "raw", wire_bytes: Optional[int] = None,
-                 root_render_fn: Optional[Callable] = None):
+                 root_render_fn: Optional[Callable] = None, shares=(1, 1)):
         import torch
         self.torch = torch
         self.W, self.H = width, height
@@ -97,8 +145,14 @@ class FrameDriver:
         # tiles: (parts, world, part_stride_bytes, W, H, B, out, stream)
         self.deinterleave_fn = deinterleave_fn
         self.dist = dist
-        self.rows = owned_rows_py(height, rank, world, block_rows)
-        self.stride = owned_rows_py(height, 0, world, block_rows)  # rank 0 owns the most
+        self.shares = tuple(shares)
+        if self.shares != (1, 1) and (wire != "tiles" or world == 1):
+            raise ValueError("unequal shares need the tiles wire (the raw rows' "
+                             "sdf_deinterleave takes the plain interleave)")
+        self.rows = owned_rows_py(height, rank, world, block_rows, self.shares)
+        # the largest part sizes every rank's buffers
+        self.stride = max(owned_rows_py(height, r, world, block_rows, self.shares)
+                          for r in range(world))
         self.gpu = getattr(device, "type", str(device)).startswith("cuda")
         self.nbuf = nbuf
         self.wire = wire if world > 1 else "raw"
@@ -109,8 +163,8 @@ class FrameDriver:
                 from .renderer import tiles_bytes
                 wire_bytes = tiles_bytes(width, self.stride)
             self.cap = wire_bytes                     # part pitch in bytes
-            # rank 0 owns the most rows, so its stream header is the longest:
-            # its data offset + the largest `used` covers every rank's stream
+            # the largest part's stream header is the longest: its data
+            # offset + the largest `used` covers every rank's stream
             self.data_off = tiles_data_offset(width, self.stride)
             self.local = [torch.zeros((self.cap,), dtype=torch.uint8, device=device)
                           for _ in range(nbuf)]
@@ -235,8 +289,8 @@ class FrameDriver:
             count = self.data_off + int(self._used(b).item())
             self.size_works[b] = None
             if self.root:
-                if self.gpu and self.asm_done[b] is not None:
-                    s.wait_event(self.asm_done[b])   # decode of i - nbuf read gathered[b]
+                # the decode of frame i - nbuf, which read gathered[b], is
+                # already on stream s, which the gather waits for
                 glist = [self.gathered[b][r * self.cap:r * self.cap + count]
                          for r in range(self.world)]
                 self.works[b] = dist.gather(self.local[b][:count], gather_list=glist, dst=0,
@@ -246,18 +300,20 @@ class FrameDriver:
                                             async_op=True)
         if self.root:
             if self.gpu:
-                with torch.cuda.stream(self.side):
+                # the decode goes on the frame's own render stream: the next
+                # render into frames[b] (frame i + nbuf) has to follow it
+                # anyway, and measured on one MI355X (tools/root_probe.py)
+                # the root's frame period is 0.074 ms this way against 0.093
+                # with the decodes on a side stream of their own
+                with torch.cuda.stream(s):
                     self.works[b].wait()
                     self.deinterleave_fn(self.gathered[b], self.world, self.cap, self.W, self.H,
-                                         self.B, self.frames[b], self.side)
-                    ev = torch.cuda.Event()
-                    ev.record(self.side)
-                    self.asm_done[b] = ev
+                                         self.B, self.frames[b], s, shares=self.shares)
             else:
                 self.works[b].wait()
                 self.works[b] = None
                 self.deinterleave_fn(self.gathered[b], self.world, self.cap, self.W, self.H,
-                                     self.B, self.frames[b], None)
+                                     self.B, self.frames[b], None, shares=self.shares)
 
     def drain(self) -> None:
         if self.wire == "tiles" and self.pending is not None:

@@ -15,12 +15,22 @@ from .scenes import Frame
 
 
 def tiling(rank: int = 0, world: int = 1, block_rows: int = 8,
-           frame_rows: bool = False) -> abi.sdf_tiling:
-    """Interleaved row-block tiling: device `rank` of `world` owns blocks
-    rank, rank + world, ...; frame_rows: write them at their
-    frame positions of a full-height buffer (SDF_TILING_FRAME_ROWS)."""
+           frame_rows: bool = False, shares: tuple[int, int] = (1, 1)) -> abi.sdf_tiling:
+    """Interleaved row-block tiling of `world` devices.
+
+    shares = (a, b): per period of P = a + b (world - 1) blocks, rank 0 owns
+    the first a blocks and rank r >= 1 the b blocks from a + b (r - 1) on
+    ((1, 1): device r owns blocks r, r + world, ...).  frame_rows: write the
+    rows at their frame positions of a full-height buffer
+    (SDF_TILING_FRAME_ROWS)."""
+    a, b = shares
+    if a < 1 or b < 1:
+        raise ValueError(f"shares must be >= 1, got {shares}")
     t = abi.sdf_tiling()
-    t.block_rows, t.first_block, t.block_stride = block_rows, rank, world
+    t.block_rows = block_rows
+    t.block_stride = a + b * (world - 1)
+    t.first_block = 0 if rank == 0 else a + b * (rank - 1)
+    t.block_run = a if rank == 0 else b
     t.flags = abi.TILING_FRAME_ROWS if frame_rows else 0
     return t
 
@@ -190,10 +200,11 @@ class Renderer:
         return out
 
     def tiles_decode(self, parts, nparts: int, part_stride: int, width: int, height: int,
-                     block_rows: int = 8, out=None, stream=None):
+                     block_rows: int = 8, out=None, stream=None, tilings=None):
         """Decode `nparts` TILES streams (uint8, pitch `part_stride` bytes; part
-        r from tiling {block_rows, r, nparts}) into a (height, width, 4)
-        float32 frame on this device (sdf_tiles_decode)."""
+        r from tiling {block_rows, r, nparts}, or from tilings[r] when given)
+        into a (height, width, 4) float32 frame on this device
+        (sdf_tiles_decode / sdf_tiles_decode_tilings)."""
         torch = self.torch
         if out is None:
             out = torch.empty((height, width, 4), dtype=torch.float32, device=self.device)
@@ -202,8 +213,17 @@ class Renderer:
                 or tuple(out.shape) != (height, width, 4) or not out.is_contiguous():
             raise ValueError("TILES parts / RGBA32F frame of the wrong size, layout or type")
         with self._on_device():
-            rc = self.lib.sdf_tiles_decode(C.c_void_p(parts.data_ptr()), nparts, part_stride,
-                                           width, height, block_rows,
-                                           C.c_void_p(out.data_ptr()), self._stream(stream))
+            if tilings is None:
+                rc = self.lib.sdf_tiles_decode(C.c_void_p(parts.data_ptr()), nparts, part_stride,
+                                               width, height, block_rows,
+                                               C.c_void_p(out.data_ptr()), self._stream(stream))
+            else:
+                if len(tilings) != nparts:
+                    raise ValueError("one tiling per part")
+                arr = (abi.sdf_tiling * nparts)(*tilings)
+                rc = self.lib.sdf_tiles_decode_tilings(C.c_void_p(parts.data_ptr()), nparts,
+                                                       part_stride, arr, width, height,
+                                                       C.c_void_p(out.data_ptr()),
+                                                       self._stream(stream))
         abi.check(rc, "sdf_tiles_decode")
         return out

@@ -159,6 +159,52 @@ def test_owned_rows_matches_oracle_and_partitions(height, world):
     assert renderer.owned_rows(height, renderer.tiling((height + 7) // 8, 1, 8)) == 0
 
 
+def tiling_rows(height, t):
+    """Frame rows a tiling owns, in packed order, straight from the
+    definition in include/sdf_abi.h (sdf_tiling)."""
+    run = max(t.block_run, 1)
+    return [y for y in range(height)
+            if y // t.block_rows >= t.first_block
+            and (y // t.block_rows - t.first_block) % t.block_stride < run]
+
+
+@pytest.mark.parametrize("height", [1, 9, 71, 270, 1080, 2160])
+@pytest.mark.parametrize("world,shares", [(2, (1, 2)), (3, (2, 3)), (4, (3, 1)), (8, (1, 2)),
+                                          (8, (1, 3)), (8, (2, 5))])
+def test_weighted_tiling_partitions_frame(height, world, shares):
+    """Unequal shares (sdf_tiling.block_run): every rank's rows as the
+    library and the oracle count them, and together exactly the frame."""
+    rows = []
+    for r in range(world):
+        t = renderer.tiling(r, world, 8, shares=shares)
+        ys = tiling_rows(height, t)
+        n = renderer.owned_rows(height, t)
+        assert n == len(ys) == oracle.owned_rows(height, t)
+        rows += ys
+    assert sorted(rows) == list(range(height))
+    # rank 0's share is a / (a + b (world - 1)) of whole periods
+    a, b = shares
+    period = 8 * (a + b * (world - 1))
+    if height % period == 0:
+        assert renderer.owned_rows(height, renderer.tiling(0, world, 8, shares=shares)) == \
+            height // period * 8 * a
+
+
+def test_tiling_run_validation():
+    lib = abi.load_library()
+    t = renderer.tiling(1, 4, 8)
+    t.block_run = t.block_stride + 1          # a run longer than its period
+    assert lib.sdf_owned_rows(100, C.byref(t)) == abi.SDF_E_INVALID_ARG
+    t.block_run = -1
+    assert lib.sdf_owned_rows(100, C.byref(t)) == abi.SDF_E_INVALID_ARG
+    t.block_run = 0                           # 0 and 1 both mean one block
+    n0 = lib.sdf_owned_rows(100, C.byref(t))
+    t.block_run = 1
+    assert lib.sdf_owned_rows(100, C.byref(t)) == n0 == len(tiling_rows(100, t))
+    with pytest.raises(ValueError):
+        renderer.tiling(0, 2, 8, shares=(0, 1))
+
+
 def test_strerror():
     lib = abi.load_library()
     for code in (abi.SDF_OK, abi.SDF_E_INVALID_ARG, abi.SDF_E_UNSUPPORTED, abi.SDF_E_HIP,

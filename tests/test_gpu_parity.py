@@ -166,6 +166,31 @@ def test_tiling_and_deinterleave_reassemble_frame(renderer, world):
     assert_parity(report(part, pst, ref, ref_st, oracle.render(f, t, twin=True)[0]), what="part")
 
 
+@pytest.mark.parametrize("world,shares", [(3, (1, 2)), (8, (1, 3))])
+def test_weighted_tiling_renders_its_rows(renderer, world, shares):
+    """Runs of blocks (sdf_tiling.block_run): each rank's packed rows are the
+    whole frame's rows it owns, bit for bit, and the oracle agrees on one."""
+    import torch
+    f = scenes.config("C3", 320, 183, precision=abi.PRECISION_FAST, pose=2)
+    whole, _ = renderer.render(f)
+    whole = whole.cpu().numpy()
+    H = f.params.height
+    for r in range(world):
+        t = R.tiling(r, world, 8, shares=shares)
+        run = max(t.block_run, 1)
+        ys = [y for y in range(H) if y // 8 >= t.first_block
+              and (y // 8 - t.first_block) % t.block_stride < run]
+        part, _ = renderer.render(f, t)
+        torch.cuda.synchronize()
+        assert part.shape[0] == len(ys)
+        assert np.array_equal(part.cpu().numpy().view(np.uint32), whole[ys].view(np.uint32))
+    t = R.tiling(1, world, 8, shares=shares)
+    part, pst = gpu(renderer, f, t)
+    ref, ref_st = oracle.render(f, t)
+    assert_parity(report(part, pst, ref, ref_st, oracle.render(f, t, twin=True)[0]),
+                  what="weighted part")
+
+
 def test_empty_tiling_is_noop(renderer):
     import torch
     f = scenes.config("REF", 64, 16)
@@ -303,14 +328,15 @@ def test_cpp_host_program(renderer, tmp_path, scene_name, cfg):
     assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
 
 
-@pytest.mark.parametrize("nproc,wire", [(2, "auto"), (3, "auto"), (2, "rgb32f")])
-def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire):
+@pytest.mark.parametrize("nproc,wire,shares", [(2, "auto", None), (3, "auto", None),
+                                               (2, "rgb32f", None), (3, "tiles", "1:2")])
+def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire, shares):
     """bench.py with 2-3 ranks sharing this GPU (gloo backend; RCCL needs one
     GPU per rank): the FrameDriver's GPU path -- alternating render streams,
     the TILES wire (auto: kernel-written compressed streams, per-frame size
-    agreement, sdf_tiles_decode on rank 0's side stream) or the RGB32F wire
-    (sdf_deinterleave) -- assembles frames bit-identical to a single-device
-    render."""
+    agreement, sdf_tiles_decode_tilings on the frame's render stream of rank
+    0, unequal row shares) or the RGB32F wire (sdf_deinterleave) --
+    assembles frames bit-identical to a single-device render."""
     import json
     import socket
     import subprocess
@@ -323,6 +349,8 @@ def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire):
            str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
            str(root / "bench.py"), "--gpus", str(nproc), "--steps", "4", "--warmup", "2",
            "--backend", "gloo", "--config", "C3", "--wire", wire, "--no-display"]
+    if shares:
+        cmd += ["--shares", shares]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -330,6 +358,8 @@ def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire):
     assert d["n_gpus"] == nproc and d["frame_verified"] is True
     assert d["config"]["wire"] == ("tiles" if wire == "auto" else wire)
     assert d["no_gather"]["value"] > 0
+    if shares:
+        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 1 / others 2")
 
 
 def turbo_ref(steps, which, max_steps):

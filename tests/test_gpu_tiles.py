@@ -151,6 +151,29 @@ def test_compression_on_the_bench_scene(renderer):
     assert bpp < 6.0
 
 
+@pytest.mark.parametrize("world,shares", [(2, (1, 2)), (3, (2, 3)), (8, (1, 3))])
+def test_weighted_tiles_decode_assembles_frame(renderer, world, shares):
+    """The frame driver's unequal shares: rank 0 renders its run of blocks in
+    place (SDF_TILING_FRAME_ROWS, its part left empty), ranks >= 1 their
+    runs as TILES streams; sdf_tiles_decode_tilings puts every row back."""
+    import torch
+    w, h = 88, 197
+    f = frame("C3", w, h, 3, abi.PRECISION_FAST, abi.FORMAT_RGBA32F)
+    whole, _ = renderer.render(f)
+    tilings = [R.tiling(r, world, 8, shares=shares) for r in range(world)]
+    stride = max(R.tiles_bytes(w, R.owned_rows(h, t)) for t in tilings)
+    out = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device=renderer.device)
+    renderer.render(f, R.tiling(0, world, 8, frame_rows=True, shares=shares), out=out)
+    parts = torch.zeros(world * stride, dtype=torch.uint8, device=renderer.device)
+    ft = frame("C3", w, h, 3, abi.PRECISION_FAST, abi.FORMAT_TILES)
+    for r in range(1, world):
+        if R.owned_rows(h, tilings[r]):
+            renderer.render(ft, tilings[r], out=parts[r * stride:(r + 1) * stride])
+    renderer.tiles_decode(parts, world, stride, w, h, out=out, tilings=tilings)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), whole.cpu().numpy())
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_frame_rows_tiling_assembles_in_place(renderer, world):
     """SDF_TILING_FRAME_ROWS: every rank's rows written at their frame

@@ -28,20 +28,20 @@ def frame_for(step):
     return scenes.config("C3", 72, 43, pose=step % 4)
 
 
-def tiles_decode_cpu(parts, world, cap, W, H, B, out, stream=None):
-    """CPU stand-in for sdf_tiles_decode: decode every rank's stream with the
-    NumPy reference and put its rows in place."""
+def tiles_decode_cpu(parts, world, cap, W, H, B, out, stream=None, shares=(1, 1)):
+    """CPU stand-in for sdf_tiles_decode(_tilings): decode every rank's
+    stream with the NumPy reference and put its rows in place."""
     p = parts.numpy()
     for r in range(world):
-        rows = owned_rows_py(H, r, world, B)
+        rows = owned_rows_py(H, r, world, B, shares)
         if rows == 0 or int(np.frombuffer(p[r * cap + 4:r * cap + 8].tobytes(), np.uint32)[0]) == 0:
             continue   # no stream (rank 0 rendered its rows in place)
         part = tiles_ref.decode(p[r * cap:(r + 1) * cap], W, rows)
-        out[torch.as_tensor(owned_row_ids(H, r, world, B))] = torch.from_numpy(part)
+        out[torch.as_tensor(owned_row_ids(H, r, world, B, shares))] = torch.from_numpy(part)
     return out
 
 
-def _worker(rank, world, port, q, wire_channels=4, direct=False):
+def _worker(rank, world, port, q, wire_channels=4, direct=False, shares=(1, 1)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -50,7 +50,7 @@ def _worker(rank, world, port, q, wire_channels=4, direct=False):
 
         def render_fn(out, stream):
             f = frame_for(step_box[0])
-            rgba, _ = oracle.render(f, R.tiling(rank, world, 8), nthreads=1)
+            rgba, _ = oracle.render(f, R.tiling(rank, world, 8, shares=shares), nthreads=1)
             if tiles:
                 st = tiles_ref.encode(rgba)
                 out[:st.size] = torch.from_numpy(st)
@@ -62,14 +62,15 @@ def _worker(rank, world, port, q, wire_channels=4, direct=False):
         def root_fn(frame, stream):
             # rank 0's rows straight into the frame (SDF_TILING_FRAME_ROWS)
             f = frame_for(step_box[0])
-            rgba, _ = oracle.render(f, R.tiling(0, world, 8), nthreads=1)
-            frame[torch.as_tensor(owned_row_ids(H, 0, world))] = torch.from_numpy(rgba)
+            rgba, _ = oracle.render(f, R.tiling(0, world, 8, shares=shares), nthreads=1)
+            frame[torch.as_tensor(owned_row_ids(H, 0, world, 8, shares))] = torch.from_numpy(rgba)
 
         if tiles:
+            big = max(owned_rows_py(H, r, world, 8, shares) for r in range(world))
             drv = FrameDriver(W, H, rank, world, torch.device("cpu"), render_fn,
                               tiles_decode_cpu, dist=dist, wire="tiles",
-                              wire_bytes=tiles_ref.capacity(W, owned_rows_py(H, 0, world)),
-                              root_render_fn=root_fn if direct else None)
+                              wire_bytes=tiles_ref.capacity(W, big),
+                              root_render_fn=root_fn if direct else None, shares=shares)
         else:
             drv = FrameDriver(W, H, rank, world, torch.device("cpu"),
                               render_fn, deinterleave_torch, dist=dist,
@@ -91,16 +92,19 @@ def _worker(rank, world, port, q, wire_channels=4, direct=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,wire,direct", [(2, 4, False), (3, 4, False), (2, 3, False),
-                                               (2, "tiles", False), (3, "tiles", True)])
-def test_frame_driver_gloo(world, wire, direct):
+@pytest.mark.parametrize("world,wire,direct,shares", [
+    (2, 4, False, (1, 1)), (3, 4, False, (1, 1)), (2, 3, False, (1, 1)),
+    (2, "tiles", False, (1, 1)), (3, "tiles", True, (1, 1)), (3, "tiles", True, (1, 2)),
+    (4, "tiles", False, (2, 3))])
+def test_frame_driver_gloo(world, wire, direct, shares):
     """wire = 3: the lossless RGB32F wire format (alpha restored on rank 0);
     "tiles": the compressed TILES streams (NumPy codec standing in for the
-    kernels), variable-length, with the per-frame size agreement."""
+    kernels), variable-length, with the per-frame size agreement; shares:
+    unequal row shares (rank 0 fewer)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire, direct))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire, direct, shares))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -111,6 +115,29 @@ def test_frame_driver_gloo(world, wire, direct):
     for i, got in frames:
         want, _ = oracle.render(frame_for(i), nthreads=1)
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), i
+
+
+@pytest.mark.parametrize("H", [1, 43, 600, 2160])
+@pytest.mark.parametrize("world,shares", [(2, (1, 2)), (8, (1, 3)), (5, (3, 2))])
+def test_share_index_math_matches_c_abi(H, world, shares):
+    seen = np.zeros(H, dtype=int)
+    for r in range(world):
+        n = owned_rows_py(H, r, world, 8, shares)
+        assert n == R.owned_rows(H, R.tiling(r, world, 8, shares=shares))
+        ids = owned_row_ids(H, r, world, 8, shares)
+        assert len(ids) == n
+        seen[ids] += 1
+    assert (seen == 1).all()
+
+
+def test_choose_shares():
+    from sdf3d_amd.multigpu import choose_shares
+    assert choose_shares(1) == (1, 1)
+    assert choose_shares(2) == (1, 1)       # root's decode is cheap next to half a frame
+    a, b = choose_shares(8)
+    assert a < b                            # rank 0 decodes 7 streams: fewer rows
+    # with a free decode the shares balance renders alone
+    assert choose_shares(8, {"render": 1.0, "render_tiles": 1.0, "decode": 0.0}) == (1, 1)
 
 
 @pytest.mark.parametrize("H", [1, 8, 43, 600, 2160])

@@ -3,8 +3,8 @@
 
 At N ranks the root renders its own rows straight into the frame
 (SDF_TILING_FRAME_ROWS) on alternating streams and decodes the N - 1 peer
-streams into the same frame on a side stream; a peer renders its share as
-TILES.  Without N GPUs the peers' streams are rendered once up front and the
+streams into the same frame (the frame driver: on the frame's own render
+stream, root_serial below); a peer renders its share as TILES.  Without N GPUs the peers' streams are rendered once up front and the
 root's loop is timed alone (the RCCL transfer itself is not included), so the
 frame period at N is bounded below by max(root, peer):
 
@@ -14,7 +14,7 @@ frame period at N is bounded below by max(root, peer):
     root_serial    both on one stream (no overlap)
     peer_tiles     one peer's share as TILES, frames on 3 streams
 
-    python tools/root_probe.py [--world 8] [--config C4] [--frames 200]
+    python tools/root_probe.py [--world 8] [--shares 1:3] [--config C4] [--frames 200]
 """
 from __future__ import annotations
 
@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--config", default="C4")
     ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--shares", default="1:1", help="rank 0 : other ranks, blocks per period")
     ap.add_argument("--only", choices=["decode", "root", "peer"], default=None,
                     help="time one leg only (for rocprofv3 counter passes)")
     args = ap.parse_args()
@@ -44,24 +45,28 @@ def main():
     W, H = f.params.width, f.params.height
     ft = f.copy()
     ft.params.output_format = abi.FORMAT_TILES
-    stride = R.tiles_bytes(W, R.owned_rows(H, R.tiling(0, N, 8)))
+    shares = tuple(int(v) for v in args.shares.split(":"))
+    tilings = [R.tiling(r, N, 8, shares=shares) for r in range(N)]
+    stride = max(R.tiles_bytes(W, R.owned_rows(H, t)) for t in tilings)
     parts = torch.zeros(N * stride, dtype=torch.uint8, device=rd.device)
     for r in range(1, N):
-        rd.render(ft, R.tiling(r, N, 8), out=parts[r * stride:(r + 1) * stride])
+        rd.render(ft, tilings[r], out=parts[r * stride:(r + 1) * stride])
     frames = [torch.empty((H, W, 4), dtype=torch.float32, device=rd.device) for _ in range(3)]
     streams = [torch.cuda.Stream() for _ in range(3)]
     side = torch.cuda.Stream()
-    t0_tiling = R.tiling(0, N, 8, frame_rows=True)
+    t0_tiling = R.tiling(0, N, 8, frame_rows=True, shares=shares)
+    # the busiest peer: the most rows
+    busiest = max(range(1, N), key=lambda r: R.owned_rows(H, tilings[r])) if N > 1 else 0
     peer_bufs = [torch.empty(stride, dtype=torch.uint8, device=rd.device) for _ in range(3)]
 
     def run(render=True, decode=True, serial=False, peer=False):
         for b in range(3):
             if peer:
-                rd.render(ft, R.tiling(1, N, 8), out=peer_bufs[b], stream=streams[b])
+                rd.render(ft, tilings[busiest], out=peer_bufs[b], stream=streams[b])
             if render:
                 rd.render(f, t0_tiling, out=frames[b], stream=streams[b])
             if decode:
-                rd.tiles_decode(parts, N, stride, W, H, 8, out=frames[b],
+                rd.tiles_decode(parts, N, stride, W, H, 8, tilings=tilings, out=frames[b],
                                 stream=streams[b] if serial else side)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -69,12 +74,12 @@ def main():
             b = i % 3
             s = streams[b]
             if peer:
-                rd.render(ft, R.tiling(1, N, 8), out=peer_bufs[b], stream=s)
+                rd.render(ft, tilings[busiest], out=peer_bufs[b], stream=s)
                 continue
             if render:
                 rd.render(f, t0_tiling, out=frames[b], stream=s)
             if decode:
-                rd.tiles_decode(parts, N, stride, W, H, 8, out=frames[b],
+                rd.tiles_decode(parts, N, stride, W, H, 8, tilings=tilings, out=frames[b],
                                 stream=s if serial else side)
         torch.cuda.synchronize()
         return round((time.perf_counter() - t0) / K * 1e3, 4)
@@ -89,7 +94,7 @@ def main():
         torch.cuda.synchronize()
         return round((time.perf_counter() - t0) / K * 1e3, 4)
 
-    out = {"config": args.config, "world": N, "frames": K}
+    out = {"config": args.config, "world": N, "shares": args.shares, "frames": K}
     if args.only:
         leg = {"decode": dict(render=False), "root": dict(), "peer": dict(render=False,
                decode=False, peer=True)}[args.only]
