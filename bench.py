@@ -66,10 +66,17 @@ def parse():
                          "and every other rank b per period of a + b (N - 1) (rank 0 "
                          "also decodes the others' streams); auto = the cost model of "
                          "multigpu.choose_shares; other wires always 1:1")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=0,
                     help="render streams / buffer sets of the frame driver (frame i on "
                          "stream i %% streams: a frame starts while the previous one's "
-                         "slowest tiles finish); 1 serialises launches (profiling)")
+                         "slowest tiles finish); 1 serialises launches (profiling); "
+                         "0 = 3 at N=1, 4 at N>1")
+    ap.add_argument("--lag", type=int, default=2,
+                    help="N>1: frames between a frame's render and its gather (the host "
+                         "reads the frame's agreed stream lengths that much later)")
+    ap.add_argument("--driver", default="native", choices=["native", "python"],
+                    help="frame loop: native = sdf_driver_* (C++, RCCL called directly); "
+                         "python = multigpu.FrameDriver over torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-stride", type=int, default=4,
                     help="CPU baseline renders every k-th 8-row block of the frame")
@@ -186,10 +193,66 @@ def main():
     t = R.tiling(rank, world, 8, shares=shares)
     t_equal = R.tiling(rank, world, 8)
     rows = R.owned_rows(H, t)
+    nbuf = args.streams or (3 if world == 1 else 4)
+    lag = min(args.lag, nbuf - 1) if nbuf > 1 else 1
+
+    open_drivers = []   # closed before the process group goes
+
+    def native_driver(fr):
+        """The C++ frame driver for frames of `fr`'s format, or None when it
+        cannot serve them (then every rank falls back to the Python driver)."""
+        from sdf3d_amd.driver import NativeFrameDriver
+        f32 = fr.copy()
+        if world > 1 or fr.params.output_format == abi.FORMAT_TILES:
+            f32.params.output_format = abi.FORMAT_RGBA32F
+        # N > 1: the TILES wire (lossless, decoded into an RGBA32F frame)
+        wire_ok = world == 1 or fr.params.output_format == abi.FORMAT_TILES
+        ok, drv = wire_ok and nbuf >= 2, None
+        if ok:
+            try:
+                drv = NativeFrameDriver(f32, rank, world, dev, shares=shares, nbuf=nbuf,
+                                        lag=lag if world > 1 else 1,
+                                        dist=dist if world > 1 else None)
+            except Exception as e:  # noqa: BLE001 - reported, then the fallback
+                log(f"[bench] rank {rank}: native driver unavailable ({e})")
+                ok = False
+        if world > 1:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0 and drv is not None:
+                drv.close()
+                drv, ok = None, False
+        if drv is not None:
+            open_drivers.append(drv)
+        return drv
 
     def timed_run(fr, steps, warmup):
-        """warmup + `steps` timed frames of `fr` through a FrameDriver; returns
+        """warmup + `steps` timed frames of `fr` through a frame driver; returns
         (max-over-ranks seconds, per-launch kernel ms list, driver)."""
+        # (gloo rehearsals share one GPU between ranks, which RCCL refuses)
+        use_native = args.driver == "native" and nbuf >= 2 and (world == 1 or
+                                                                  args.backend == "nccl")
+        drv = native_driver(fr) if use_native else None
+        if drv is not None:
+            for _ in range(warmup):
+                drv.step()
+            drv.drain()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                drv.step()
+            drv.drain()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+            if world > 1:
+                e = torch.tensor([el], dtype=torch.float64, device=dev)
+                dist.all_reduce(e, op=dist.ReduceOp.MAX)
+                el = float(e.item())
+            return el, [], drv
         tiles = fr.params.output_format == abi.FORMAT_TILES
         tr = t if tiles else t_equal
 
@@ -213,13 +276,14 @@ def main():
 
             drv = FrameDriver(W, H, rank, world, dev, render_fn, tiles_fn,
                               dist=dist if world > 1 else None, wire="tiles",
-                              nbuf=args.streams, root_render_fn=root_fn, shares=shares)
+                              nbuf=nbuf, root_render_fn=root_fn, shares=shares,
+                              lag=lag)
         else:
             def deint_fn(parts, nparts, stride, w, h, b, out, stream):
                 rd.deinterleave(parts, nparts, stride, w, h, b, out=out, stream=stream)
 
             drv = FrameDriver(W, H, rank, world, dev, render_fn, deint_fn,
-                              dist=dist if world > 1 else None, nbuf=args.streams,
+                              dist=dist if world > 1 else None, nbuf=nbuf,
                               dtype=R.torch_dtype(fr.params.output_format),
                               wire_channels=R.channels(fr.params.output_format))
         k = steps + warmup
@@ -260,7 +324,7 @@ def main():
         display = {"format": "rgba8", "value": round(W * H * args.steps / el8 / 1e6, 3),
                    "fps": round(args.steps / el8, 2),
                    "ms_per_step": round(el8 / args.steps * 1e3, 4),
-                   "render_ms_pipelined": round(sum(km8) / len(km8), 4)}
+                   "render_ms_pipelined": round(sum(km8) / len(km8), 4) if km8 else None}
 
     # the same frames without the gather (scaling with and
     # without it): each rank renders its blocks only, max over ranks
@@ -296,7 +360,8 @@ def main():
         whole = scenes.config(args.config, precision=prec, pose=args.pose)
         whole.params.output_format = abi.FORMAT_NAMES[args.format]
         ref, _ = rd.render(whole)
-        got = drv.frame(k_steps - 1)
+        got = (drv.read_frame(k_steps - 1) if hasattr(drv, "read_frame")
+               else drv.frame(k_steps - 1))
         torch.cuda.synchronize(dev)
         verified = bool(torch.equal(got.view(torch.uint8), ref.view(torch.uint8)))
         log(f"[bench] assembled frame == single-device frame: {verified}")
@@ -321,6 +386,15 @@ def main():
     del kbuf
     flops = rank_flops(frame, t, args.pose)
 
+    native = hasattr(drv, "read_frame")
+    driver_desc = ("native (sdf_driver_*, C++)" if native
+                   else "python (multigpu.FrameDriver, torch.distributed)")
+    if native:
+        gather_desc = ("RCCL all-gather of the TILES stream lengths + RCCL send/recv of "
+                       "exactly those bytes to rank 0 + sdf_tiles_decode_tilings")
+    else:
+        gather_desc = (f"{'RCCL' if args.backend == 'nccl' else 'gloo'} gather to rank 0 + "
+                       + ("sdf_tiles_decode_tilings" if wire == "tiles" else "sdf_deinterleave"))
     if rank == 0:
         value = W * H * args.steps / elapsed / 1e6
         out = {
@@ -336,10 +410,9 @@ def main():
                        "tiling": (f"8-row blocks, rank 0 {shares[0]} / others {shares[1]} per "
                                   f"period of {shares[0] + shares[1] * (world - 1)}"
                                   if world > 1 else "whole frame"),
-                       "gather": (f"{'RCCL' if args.backend == 'nccl' else 'gloo'} gather to "
-                                  "rank 0 + " + ("sdf_tiles_decode_tilings" if wire == "tiles"
-                                                 else "sdf_deinterleave"))
-                       if world > 1 else None},
+                       "gather": gather_desc if world > 1 else None,
+                       "driver": driver_desc,
+                       "streams": nbuf, "lag": lag if world > 1 else None},
             "fps": round(args.steps / elapsed, 2),
             "frame_verified": verified,
             "display_rgba8": display,
@@ -379,6 +452,8 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    for d in open_drivers:
+        d.close()
     if world > 1:
         dist.destroy_process_group()
 

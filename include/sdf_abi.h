@@ -25,6 +25,11 @@
  *                    shader's `fragment_color` (:12, :210) as float RGBA.
  *   sdf_deinterleave() gathers per-device row blocks into one frame (new: the
  *                    reference has a single GL context, main.cpp:48,53).
+ *   sdf_driver_*()   the multi-device frame loop: the reference's per-frame
+ *                    `gl->plot` loop (main.cpp:87-98) run across the GPUs of
+ *                    one node, every rank rendering its row blocks and rank 0
+ *                    assembling the frame over RCCL (new: the reference has a
+ *                    single GL context, main.cpp:48,53).
  *   sdf_strerror()   error text (the reference has none: main.cpp:109).
  *
  * Conventions
@@ -51,7 +56,7 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 3
+#define SDF_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -59,6 +64,8 @@ extern "C" {
 #define SDF_E_UNSUPPORTED   -2  /* valid request this build cannot serve       */
 #define SDF_E_HIP           -3  /* a HIP runtime call failed                   */
 #define SDF_E_NO_DEVICE     -4  /* no gfx950 device visible                    */
+#define SDF_E_COMM          -5  /* RCCL could not be loaded or a collective failed */
+#define SDF_E_TIMEOUT       -6  /* the frame driver waited longer than its limit */
 
 /* ---- scene description -------------------------------------------------- */
 #define SDF_MAX_PRIMS 16
@@ -345,6 +352,73 @@ int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_
 /* Number of scene signatures compiled at run time in this process (see
  * SDF_DISPATCH_AUTO). */
 int sdf_jit_count(void);
+
+/* ---- multi-device frame driver ----------------------------------------------
+ * One process per GPU.  Every rank renders its row blocks of each frame
+ * (tiling with shares: rank 0 `share_root` blocks and every other rank
+ * `share_peer` blocks per period of share_root + share_peer * (world - 1))
+ * as a TILES stream; rank 0 renders its own rows straight into the frame and
+ * assembles the rest: an RCCL all-gather of the streams' lengths, RCCL
+ * point-to-point transfers of exactly those bytes to rank 0, and
+ * sdf_tiles_decode_tilings into the frame -- bit-identical to a one-device
+ * render.  Frames rotate over `nbuf` buffer sets, one HIP stream each; frame
+ * i is shipped `lag` frames after its render (the host reads its agreed
+ * lengths from pinned memory, without stalling the queue when lag >= 2).
+ * The collectives run on two communicators (lengths; data), each on its own
+ * stream, issued in the same order on every rank.
+ *
+ * RCCL is loaded at run time from `rccl_path` (the librccl.so this process
+ * already uses, e.g. PyTorch's, so one RCCL instance serves both); the
+ * caller exchanges the 128-byte unique id of each communicator (rank 0 makes
+ * it with sdf_comm_unique_id) through its own channel.
+ * world == 1 needs no communicator: frames render whole, nothing is shipped. */
+#define SDF_COMM_ID_BYTES 128
+typedef struct sdf_comm sdf_comm;
+typedef struct sdf_driver sdf_driver;
+
+int sdf_comm_unique_id(const char* rccl_path, void* id /* SDF_COMM_ID_BYTES */);
+/* Collective over nranks processes (blocks until all have joined); the
+ * current HIP device is the communicator's. */
+int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
+                    sdf_comm** comm);
+int sdf_comm_destroy(sdf_comm* comm);
+
+/* SDF_DRIVER_ROOT_AS_PEER: rank 0 ships its rows as a TILES stream to itself
+ * like every other rank (probes of one rank's full per-frame cost on one
+ * GPU, world == 1 included). */
+#define SDF_DRIVER_ROOT_AS_PEER 0x1
+typedef struct {
+  int32_t rank, world;
+  int32_t share_root, share_peer; /* blocks per period (>= 1; 1:1 = plain interleave) */
+  int32_t nbuf;                   /* buffer sets / render streams, 2 .. 16             */
+  int32_t lag;                    /* frames from render to gather, 1 .. nbuf - 1      */
+  int32_t flags;                  /* SDF_DRIVER_*                                     */
+  int32_t timeout_ms;             /* host waits give up after this (<= 0: 60000)      */
+} sdf_driver_config;
+
+/* The frame format is params->output_format (RGBA32F at world > 1: the wire
+ * is lossless TILES).  size_comm / data_comm: two communicators over the
+ * same `world` ranks (NULL when world == 1 without ROOT_AS_PEER). */
+int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                      const sdf_material* material, const sdf_params* params,
+                      const sdf_driver_config* config, sdf_comm* size_comm, sdf_comm* data_comm,
+                      sdf_driver** driver);
+/* Camera of the frames stepped from now on (the arcball V_mat of main.cpp:93-94). */
+int sdf_driver_set_camera(sdf_driver* driver, const sdf_camera* camera);
+/* Enqueue the next frame (index returned in *frame_index, may be NULL). */
+int sdf_driver_step(sdf_driver* driver, int64_t* frame_index);
+/* Ship every rendered frame and wait until all work of this rank is done. */
+int sdf_driver_drain(sdf_driver* driver);
+/* Rank 0 (or world 1): device pointer of frame `index`'s framebuffer
+ * (height * width pixels), one of the last nbuf frames, assembled once it
+ * has been shipped (after sdf_driver_drain for the last `lag`). */
+int sdf_driver_frame(sdf_driver* driver, int64_t index, void** rgba);
+/* Copy frame `index` (as sdf_driver_frame) into the caller's device buffer
+ * `dst` of `bytes` (>= the frame's size), asynchronously on `stream` after
+ * all work queued for that frame. */
+int sdf_driver_read_frame(sdf_driver* driver, int64_t index, void* dst, int64_t bytes,
+                          void* stream);
+int sdf_driver_destroy(sdf_driver* driver);
 
 /* Short description of a status code. */
 const char* sdf_strerror(int code);

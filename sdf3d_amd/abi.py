@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 3
+SDF_ABI_VERSION = 4
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -20,6 +20,10 @@ SDF_E_INVALID_ARG = -1
 SDF_E_UNSUPPORTED = -2
 SDF_E_HIP = -3
 SDF_E_NO_DEVICE = -4
+SDF_E_COMM = -5
+SDF_E_TIMEOUT = -6
+COMM_ID_BYTES = 128
+DRIVER_ROOT_AS_PEER = 0x1
 
 # primitive kinds
 PRIM_SPHERE, PRIM_PLANE, PRIM_BOX, PRIM_ROUND_BOX, PRIM_TORUS, PRIM_CAPSULE, PRIM_CYLINDER = range(7)
@@ -89,9 +93,16 @@ class sdf_tiling(C.Structure):
                 ("block_run", C.c_int32)]
 
 
+class sdf_driver_config(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("share_root", C.c_int32),
+                ("share_peer", C.c_int32), ("nbuf", C.c_int32), ("lag", C.c_int32),
+                ("flags", C.c_int32), ("timeout_ms", C.c_int32)]
+
+
 STRUCT_SIZES = {
     "sdf_primitive": 64, "sdf_scene": 8 + 64 * SDF_MAX_PRIMS + 32, "sdf_camera": 88,
     "sdf_light": 32, "sdf_material": 40, "sdf_params": 80, "sdf_tiling": 20,
+    "sdf_driver_config": 32,
 }
 
 # every entry point of include/sdf_abi.h: name -> (restype, argtypes)
@@ -116,6 +127,20 @@ SIGNATURES = {
                                            C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                               C.c_void_p, C.c_void_p]),
+    "sdf_comm_unique_id": (C.c_int, [C.c_char_p, C.c_void_p]),
+    "sdf_comm_create": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32,
+                                  _P(C.c_void_p)]),
+    "sdf_comm_destroy": (C.c_int, [C.c_void_p]),
+    "sdf_driver_create": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light),
+                                    _P(sdf_material), _P(sdf_params), _P(sdf_driver_config),
+                                    C.c_void_p, C.c_void_p, _P(C.c_void_p)]),
+    "sdf_driver_set_camera": (C.c_int, [C.c_void_p, _P(sdf_camera)]),
+    "sdf_driver_step": (C.c_int, [C.c_void_p, _P(C.c_int64)]),
+    "sdf_driver_drain": (C.c_int, [C.c_void_p]),
+    "sdf_driver_frame": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_void_p)]),
+    "sdf_driver_read_frame": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                        C.c_void_p]),
+    "sdf_driver_destroy": (C.c_int, [C.c_void_p]),
     "sdf_strerror": (C.c_char_p, [C.c_int]),
 }
 

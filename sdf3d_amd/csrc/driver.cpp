@@ -1,0 +1,535 @@
+// driver.cpp -- the native multi-device frame driver (include/sdf_abi.h
+// sdf_comm_* / sdf_driver_*).
+//
+// The reference draws one frame per iteration of its host loop
+// (/root/reference/Code/src/main.cpp:87-98, `gl->plot` at :95) on one GL
+// context.  Here every rank of a node renders its row blocks of each frame
+// and rank 0 assembles the frame; this file is the per-frame loop around the
+// kernels, in C++ so that the host cost per frame stays far below the GPU's
+// (at N = 8 a rank's share of the 4K frame renders in ~0.06 ms; the same
+// loop through torch.distributed costs ~0.12 ms of host time per frame,
+// tools/driver_probe.py).
+//
+// Per frame i on rank r (b = i mod nbuf):
+//   rs[b]  render(i): rank 0 its rows into frame[b] in place, the others
+//          their TILES stream into local[b]                     -> ev_render[b]
+//   ss     wait ev_render[b]; all-gather of the stream lengths (size comm);
+//          copy to pinned host memory                           -> ev_size[b]
+// and `lag` frames later, ship(i):
+//   host   wait ev_size[b]: every rank's length of frame i
+//   ds     wait ev_render[b]; group { send local[b] (lengths exact) to rank 0
+//          | rank 0: recv from every peer into gathered[b] }     -> ev_gather[b]
+//   rs[b]  wait ev_gather[b]; rank 0: decode gathered[b] into frame[b]
+// Every use of buffer set b is ordered on rs[b] (the next render into it
+// follows the decode / waits for the send), each communicator is used from
+// one stream only, and every rank issues the same collectives in the same
+// order, so no collective can overtake another.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: functions are resolved in the RCCL loaded at run time
+#include <sched.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sdf_abi.h"
+#include "host_api.h"
+#include "kernel_args.h"
+
+namespace {
+
+struct Rccl {
+  void* handle = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+};
+
+// One Rccl per library path, loaded once: dlopen of a library the process
+// already has mapped (PyTorch's librccl.so) returns that same instance.
+Rccl* load_rccl(const char* path) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::string, Rccl*>> loaded;
+  std::lock_guard<std::mutex> lock(mu);
+  const std::string key = path && *path ? path : "librccl.so";
+  for (auto& e : loaded)
+    if (e.first == key) return e.second;
+  void* h = dlopen(key.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!h) return nullptr;
+  Rccl* r = new Rccl();
+  r->handle = h;
+  bool ok = true;
+  auto sym = [&](auto& fn, const char* name) {
+    fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+    ok = ok && fn != nullptr;
+  };
+  sym(r->GetUniqueId, "ncclGetUniqueId");
+  sym(r->CommInitRank, "ncclCommInitRank");
+  sym(r->CommDestroy, "ncclCommDestroy");
+  sym(r->CommAbort, "ncclCommAbort");
+  sym(r->CommGetAsyncError, "ncclCommGetAsyncError");
+  sym(r->AllGather, "ncclAllGather");
+  sym(r->Send, "ncclSend");
+  sym(r->Recv, "ncclRecv");
+  sym(r->GroupStart, "ncclGroupStart");
+  sym(r->GroupEnd, "ncclGroupEnd");
+  if (!ok) {
+    delete r;
+    dlclose(h);
+    return nullptr;
+  }
+  loaded.emplace_back(key, r);
+  return r;
+}
+
+}  // namespace
+
+struct sdf_comm {
+  Rccl* api;
+  ncclComm_t comm;
+  int nranks, rank, device;
+};
+
+struct sdf_driver {
+  int dev = 0;
+  int W = 0, H = 0, rank = 0, world = 1, nbuf = 0, lag = 1, flags = 0, timeout_ms = 60000;
+  bool collectives = false;  // anything shipped at all
+  bool sender = false;       // this rank ships a TILES stream
+  bool root = false;
+  int format = SDF_FORMAT_RGBA32F;
+  sdf_comm* size_comm = nullptr;
+  sdf_comm* data_comm = nullptr;
+  sdf_scene scene;
+  sdf_light light;
+  sdf_material material;
+  sdf_params params;
+  sdf_camera camera;
+  std::vector<sdf_tiling> tilings;  // every rank's share (packed)
+  std::vector<int> rows;
+  std::vector<long long> data_off, stream_end;
+  std::vector<char> sends;          // rank r ships a stream
+  long long pitch = 0;              // gathered part pitch
+  std::vector<void*> local, frames, gathered;
+  int32_t* sizes_dev = nullptr;
+  int32_t* sizes_host = nullptr;
+  int32_t* zero_dev = nullptr;
+  std::vector<sdf::RenderPlan> plan_send, plan_frame;
+  sdf::DecodeParts decode{};
+  std::vector<hipStream_t> rs;
+  hipStream_t ss = nullptr, ds = nullptr;
+  std::vector<hipEvent_t> ev_render, ev_size, ev_gather;
+  std::deque<long long> pending;
+  long long next = 0;
+  int error = SDF_OK;  // sticky: a failed driver refuses further frames
+};
+
+namespace {
+
+int hip_ok(hipError_t e) { return e == hipSuccess ? SDF_OK : SDF_E_HIP; }
+int nccl_ok(ncclResult_t e) { return e == ncclSuccess ? SDF_OK : SDF_E_COMM; }
+
+int fail(sdf_driver* d, int rc) {
+  if (rc != SDF_OK && d->error == SDF_OK) d->error = rc;
+  return rc;
+}
+
+// Abort the communicators so that no rank blocks forever on a peer that
+// failed: the process can then report the error and exit.
+void abort_comms(sdf_driver* d) {
+  for (sdf_comm* c : {d->size_comm, d->data_comm})
+    if (c && c->comm) {
+      c->api->CommAbort(c->comm);
+      c->comm = nullptr;
+    }
+}
+
+// Wait for `done()` on the host, polling; gives up after the driver's limit
+// or at the first asynchronous RCCL error.
+template <class Query>
+int host_wait(sdf_driver* d, Query done) {
+  hipError_t q = done();
+  if (q == hipSuccess) return SDF_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned n = 0; q == hipErrorNotReady; q = done(), ++n) {
+    if ((n & 1023) == 1023) {
+      for (sdf_comm* c : {d->size_comm, d->data_comm}) {
+        ncclResult_t ae = ncclSuccess;
+        if (c && c->comm && c->api->CommGetAsyncError(c->comm, &ae) == ncclSuccess &&
+            ae != ncclSuccess && ae != ncclInProgress) {
+          abort_comms(d);
+          return fail(d, SDF_E_COMM);
+        }
+      }
+      const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                          std::chrono::steady_clock::now() - t0).count();
+      if (ms > d->timeout_ms) {
+        abort_comms(d);
+        return fail(d, SDF_E_TIMEOUT);
+      }
+    }
+    sched_yield();
+  }
+  return fail(d, hip_ok(q));
+}
+
+int wait_event(sdf_driver* d, hipEvent_t e) {
+  return host_wait(d, [e] { return hipEventQuery(e); });
+}
+
+// ship(j): the agreed lengths are on the host; move the streams to rank 0
+// and decode them there.
+int ship(sdf_driver* d, long long j) {
+  const int b = (int)(j % d->nbuf);
+  int rc = wait_event(d, d->ev_size[b]);
+  if (rc != SDF_OK) return rc;
+  const int32_t* sz = d->sizes_host + (size_t)b * d->world;
+  for (int r = 0; r < d->world; ++r)
+    if (d->sends[r] && (sz[r] < 0 || d->data_off[r] + sz[r] > d->stream_end[r]))
+      return fail(d, SDF_E_COMM);  // a length no stream of that rank can have
+  rc = hip_ok(hipStreamWaitEvent(d->ds, d->ev_render[b], 0));
+  if (rc != SDF_OK) return fail(d, rc);
+  const Rccl& R = *d->data_comm->api;
+  ncclComm_t comm = d->data_comm->comm;
+  rc = nccl_ok(R.GroupStart());
+  if (rc == SDF_OK && d->sender)
+    rc = nccl_ok(R.Send(d->local[b], (size_t)(d->data_off[d->rank] + sz[d->rank]), ncclUint8, 0,
+                        comm, d->ds));
+  if (d->root)
+    for (int r = 0; r < d->world && rc == SDF_OK; ++r)
+      if (d->sends[r])
+        rc = nccl_ok(R.Recv(static_cast<char*>(d->gathered[b]) + (size_t)r * d->pitch,
+                            (size_t)(d->data_off[r] + sz[r]), ncclUint8, r, comm, d->ds));
+  const int rc_end = nccl_ok(R.GroupEnd());
+  if (rc == SDF_OK) rc = rc_end;
+  if (rc != SDF_OK) return fail(d, rc);
+  rc = hip_ok(hipEventRecord(d->ev_gather[b], d->ds));
+  if (rc == SDF_OK) rc = hip_ok(hipStreamWaitEvent(d->rs[b], d->ev_gather[b], 0));
+  if (rc == SDF_OK && d->root)
+    rc = hip_ok((hipError_t)sdf::launch_tiles_decode(d->decode, d->frames[b], d->gathered[b],
+                                                     d->rs[b]));
+  return fail(d, rc);
+}
+
+void release(sdf_driver* d) {
+  (void)hipSetDevice(d->dev);
+  for (auto* v : {&d->local, &d->frames, &d->gathered})
+    for (void* p : *v)
+      if (p) (void)hipFree(p);
+  if (d->sizes_dev) (void)hipFree(d->sizes_dev);
+  if (d->zero_dev) (void)hipFree(d->zero_dev);
+  if (d->sizes_host) (void)hipHostFree(d->sizes_host);
+  for (hipStream_t s : d->rs)
+    if (s) (void)hipStreamDestroy(s);
+  if (d->ss) (void)hipStreamDestroy(d->ss);
+  if (d->ds) (void)hipStreamDestroy(d->ds);
+  for (auto* v : {&d->ev_render, &d->ev_size, &d->ev_gather})
+    for (hipEvent_t e : *v)
+      if (e) (void)hipEventDestroy(e);
+  delete d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdf_comm_unique_id(const char* rccl_path, void* id) {
+  if (!id) return SDF_E_INVALID_ARG;
+  Rccl* R = load_rccl(rccl_path);
+  if (!R) return SDF_E_COMM;
+  ncclUniqueId uid;
+  if (R->GetUniqueId(&uid) != ncclSuccess) return SDF_E_COMM;
+  std::memcpy(id, &uid, sizeof(uid));
+  return SDF_OK;
+}
+
+int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
+                    sdf_comm** comm) {
+  if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return SDF_E_INVALID_ARG;
+  *comm = nullptr;
+  Rccl* R = load_rccl(rccl_path);
+  if (!R) return SDF_E_COMM;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return SDF_E_NO_DEVICE;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  if (R->CommInitRank(&c, nranks, uid, rank) != ncclSuccess) return SDF_E_COMM;
+  *comm = new sdf_comm{R, c, nranks, rank, dev};
+  return SDF_OK;
+}
+
+int sdf_comm_destroy(sdf_comm* comm) {
+  if (!comm) return SDF_OK;
+  int rc = SDF_OK;
+  if (comm->comm) rc = nccl_ok(comm->api->CommDestroy(comm->comm));
+  delete comm;
+  return rc;
+}
+
+int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                      const sdf_material* material, const sdf_params* params,
+                      const sdf_driver_config* config, sdf_comm* size_comm, sdf_comm* data_comm,
+                      sdf_driver** driver) {
+  if (!config || !driver || !params) return SDF_E_INVALID_ARG;
+  *driver = nullptr;
+  const sdf_driver_config& c = *config;
+  if (c.world < 1 || c.world > SDF_MAX_DECODE_PARTS || c.rank < 0 || c.rank >= c.world ||
+      c.share_root < 1 || c.share_peer < 1 || c.nbuf < 2 || c.nbuf > 16 || c.lag < 1 ||
+      c.lag > c.nbuf - 1 || (c.flags & ~SDF_DRIVER_ROOT_AS_PEER) != 0)
+    return SDF_E_INVALID_ARG;
+  const bool peer_root = (c.flags & SDF_DRIVER_ROOT_AS_PEER) != 0;
+  const bool collectives = c.world > 1 || peer_root;
+  if (collectives) {
+    if (!size_comm || !data_comm || size_comm == data_comm || !size_comm->comm ||
+        !data_comm->comm || size_comm->nranks != c.world || data_comm->nranks != c.world ||
+        size_comm->rank != c.rank || data_comm->rank != c.rank)
+      return SDF_E_INVALID_ARG;
+    if (params->output_format != SDF_FORMAT_RGBA32F) return SDF_E_UNSUPPORTED;
+  } else if (params->output_format == SDF_FORMAT_TILES) {
+    return SDF_E_UNSUPPORTED;
+  }
+  int rc = sdf_validate(scene, camera, light, material, params, nullptr);
+  if (rc != SDF_OK) return rc;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return SDF_E_NO_DEVICE;
+
+  sdf_driver* d = new sdf_driver();
+  d->dev = dev;
+  d->W = params->width;
+  d->H = params->height;
+  d->rank = c.rank;
+  d->world = c.world;
+  d->nbuf = c.nbuf;
+  d->lag = c.lag;
+  d->flags = c.flags;
+  d->timeout_ms = c.timeout_ms > 0 ? c.timeout_ms : 60000;
+  d->collectives = collectives;
+  d->root = c.rank == 0;
+  d->format = params->output_format;
+  d->size_comm = size_comm;
+  d->data_comm = data_comm;
+  d->scene = *scene;
+  d->light = *light;
+  d->material = *material;
+  d->params = *params;
+  d->camera = *camera;
+
+  // every rank's share: rank 0 a blocks, the others b, per period a + b (N - 1)
+  const int a = c.share_root, bsh = c.share_peer, period = a + bsh * (c.world - 1);
+  for (int r = 0; r < c.world; ++r) {
+    sdf_tiling t{8, r == 0 ? 0 : a + bsh * (r - 1), period, 0, r == 0 ? a : bsh};
+    if (c.world == 1) t = sdf_tiling{8, 0, 1, 0, 1};
+    const int n = sdf::count_rows(d->H, t);
+    if (n < 0) {
+      release(d);
+      return SDF_E_INVALID_ARG;
+    }
+    const sdf::TilesLayout L(int64_t((d->W + 7) / 8) * ((n + 7) / 8));
+    d->tilings.push_back(t);
+    d->rows.push_back(n);
+    d->data_off.push_back((long long)L.data);
+    d->stream_end.push_back((long long)L.stream_end);
+    d->sends.push_back(collectives && (r != 0 || peer_root) && n > 0);
+    d->pitch = std::max(d->pitch, (long long)((L.stream_end + 255) / 256 * 256));
+  }
+  d->sender = d->sends[c.rank] != 0;
+
+  sdf_params pf = *params;  // the frame's own rows / whole frames
+  sdf_params pt = *params;  // the wire
+  pt.output_format = SDF_FORMAT_TILES;
+  const size_t frame_bytes = (size_t)d->W * d->H * (size_t)sdf_format_bytes(pf.output_format);
+  const size_t local_bytes = (size_t)sdf_tiles_bytes(d->W, d->rows[c.rank]);
+  auto alloc = [&](void** p, size_t n) {
+    return rc == SDF_OK ? (rc = hip_ok(hipMalloc(p, n ? n : 16))) : rc;
+  };
+  d->rs.assign(c.nbuf, nullptr);
+  d->ev_render.assign(c.nbuf, nullptr);
+  d->ev_size.assign(c.nbuf, nullptr);
+  d->ev_gather.assign(c.nbuf, nullptr);
+  for (int b = 0; b < c.nbuf && rc == SDF_OK; ++b) {
+    rc = hip_ok(hipStreamCreateWithFlags(&d->rs[b], hipStreamNonBlocking));
+    for (auto* v : {&d->ev_render, &d->ev_size, &d->ev_gather})
+      if (rc == SDF_OK) rc = hip_ok(hipEventCreateWithFlags(&(*v)[b], hipEventDisableTiming));
+  }
+  if (rc == SDF_OK) rc = hip_ok(hipStreamCreateWithFlags(&d->ss, hipStreamNonBlocking));
+  if (rc == SDF_OK) rc = hip_ok(hipStreamCreateWithFlags(&d->ds, hipStreamNonBlocking));
+  d->local.assign(c.nbuf, nullptr);
+  d->frames.assign(c.nbuf, nullptr);
+  d->gathered.assign(c.nbuf, nullptr);
+  d->plan_send.resize(c.nbuf);
+  d->plan_frame.resize(c.nbuf);
+  for (int b = 0; b < c.nbuf && rc == SDF_OK; ++b) {
+    if (d->sender) {
+      alloc(&d->local[b], local_bytes);
+      // the header of a stream no render writes (0 rows) must read used = 0
+      if (rc == SDF_OK) rc = hip_ok(hipMemset(d->local[b], 0, 64));
+      if (rc == SDF_OK)
+        rc = sdf::make_render_plan(scene, camera, light, material, &pt, &d->tilings[c.rank],
+                                   d->local[b], nullptr, &d->plan_send[b]);
+    }
+    if (d->root) {
+      alloc(&d->frames[b], frame_bytes);
+      if (collectives) {
+        // part r of gathered[b] at r * pitch; parts nobody sends keep a
+        // zero header (ntiles = 0: skipped by the decode)
+        alloc(&d->gathered[b], (size_t)d->pitch * c.world);
+        if (rc == SDF_OK)
+          rc = hip_ok(hipMemset(d->gathered[b], 0, (size_t)d->pitch * c.world));
+      }
+      if (rc == SDF_OK && !d->sender) {
+        // rank 0's own rows straight into the frame (whole frames at world 1)
+        sdf_tiling t = d->tilings[0];
+        if (collectives) t.flags = SDF_TILING_FRAME_ROWS;
+        rc = sdf::make_render_plan(scene, camera, light, material, &pf, &t, d->frames[b],
+                                   nullptr, &d->plan_frame[b]);
+      }
+    }
+  }
+  if (collectives && rc == SDF_OK) {
+    alloc((void**)&d->sizes_dev, sizeof(int32_t) * c.nbuf * c.world);
+    alloc((void**)&d->zero_dev, 64);
+    if (rc == SDF_OK) rc = hip_ok(hipMemset(d->zero_dev, 0, 64));
+    if (rc == SDF_OK)
+      rc = hip_ok(hipHostMalloc((void**)&d->sizes_host, sizeof(int32_t) * c.nbuf * c.world,
+                                hipHostMallocDefault));
+    d->decode.nparts = c.world;
+    d->decode.width = d->W;
+    d->decode.height = d->H;
+    d->decode.part_stride = d->pitch;
+    for (int r = 0; r < c.world; ++r) {
+      const sdf_tiling& t = d->tilings[r];
+      d->decode.rows[r] = d->rows[r];
+      d->decode.first_block[r] = t.first_block;
+      d->decode.block_stride[r] = t.block_stride;
+      d->decode.block_rows[r] = t.block_rows;
+      d->decode.chunk_rows[r] = t.block_rows * sdf::tiling_run(t);
+    }
+  }
+  if (rc == SDF_OK) rc = hip_ok(hipDeviceSynchronize());  // memsets done
+  if (rc != SDF_OK) {
+    release(d);
+    return rc;
+  }
+  *driver = d;
+  return SDF_OK;
+}
+
+int sdf_driver_set_camera(sdf_driver* d, const sdf_camera* camera) {
+  if (!d) return SDF_E_INVALID_ARG;
+  const int rc = sdf_validate(&d->scene, camera, &d->light, &d->material, &d->params, nullptr);
+  if (rc != SDF_OK) return rc;
+  d->camera = *camera;
+  for (auto* v : {&d->plan_send, &d->plan_frame})
+    for (sdf::RenderPlan& p : *v)
+      if (p.rows > 0) sdf::plan_set_camera(&p, camera);
+  return SDF_OK;
+}
+
+int sdf_driver_step(sdf_driver* d, int64_t* frame_index) {
+  if (!d) return SDF_E_INVALID_ARG;
+  if (d->error != SDF_OK) return d->error;
+  if (hipSetDevice(d->dev) != hipSuccess) return fail(d, SDF_E_HIP);
+  const long long i = d->next;
+  const int b = (int)(i % d->nbuf);
+  hipStream_t s = d->rs[b];
+  int rc = SDF_OK;
+  if (d->sender) rc = sdf::launch_render_plan(d->plan_send[b], s);
+  if (rc == SDF_OK && d->root && !d->sender) rc = sdf::launch_render_plan(d->plan_frame[b], s);
+  if (rc != SDF_OK) return fail(d, rc);
+  if (frame_index) *frame_index = i;
+  d->next = i + 1;
+  if (!d->collectives) return SDF_OK;
+  rc = hip_ok(hipEventRecord(d->ev_render[b], s));
+  if (rc != SDF_OK) return fail(d, rc);
+  // frame i - lag: its lengths are on the host by now (lag >= 2: long since)
+  if ((int)d->pending.size() >= d->lag) {
+    const long long j = d->pending.front();
+    d->pending.pop_front();
+    rc = ship(d, j);
+    if (rc != SDF_OK) return rc;
+  }
+  // the ranks' stream lengths of frame i, to every rank
+  rc = hip_ok(hipStreamWaitEvent(d->ss, d->ev_render[b], 0));
+  if (rc != SDF_OK) return fail(d, rc);
+  int32_t* sz = d->sizes_dev + (size_t)b * d->world;
+  rc = nccl_ok(d->size_comm->api->AllGather(d->sender ? d->local[b] : (void*)d->zero_dev, sz, 1,
+                                            ncclInt32, d->size_comm->comm, d->ss));
+  if (rc == SDF_OK)
+    rc = hip_ok(hipMemcpyAsync(d->sizes_host + (size_t)b * d->world, sz,
+                               sizeof(int32_t) * d->world, hipMemcpyDeviceToHost, d->ss));
+  if (rc == SDF_OK) rc = hip_ok(hipEventRecord(d->ev_size[b], d->ss));
+  if (rc != SDF_OK) return fail(d, rc);
+  d->pending.push_back(i);
+  return SDF_OK;
+}
+
+int sdf_driver_drain(sdf_driver* d) {
+  if (!d) return SDF_E_INVALID_ARG;
+  if (d->error != SDF_OK) return d->error;
+  if (hipSetDevice(d->dev) != hipSuccess) return fail(d, SDF_E_HIP);
+  while (!d->pending.empty()) {
+    const long long j = d->pending.front();
+    d->pending.pop_front();
+    const int rc = ship(d, j);
+    if (rc != SDF_OK) return rc;
+  }
+  std::vector<hipStream_t> all = d->rs;
+  all.push_back(d->ss);
+  all.push_back(d->ds);
+  for (hipStream_t s : all) {
+    const int rc = host_wait(d, [s] { return hipStreamQuery(s); });
+    if (rc != SDF_OK) return rc;
+  }
+  return SDF_OK;
+}
+
+int sdf_driver_frame(sdf_driver* d, int64_t index, void** rgba) {
+  if (!d || !rgba) return SDF_E_INVALID_ARG;
+  *rgba = nullptr;
+  if (!d->root || index < 0 || index >= d->next || index < d->next - d->nbuf)
+    return SDF_E_INVALID_ARG;
+  *rgba = d->frames[index % d->nbuf];
+  return SDF_OK;
+}
+
+int sdf_driver_read_frame(sdf_driver* d, int64_t index, void* dst, int64_t bytes, void* stream) {
+  void* src = nullptr;
+  int rc = sdf_driver_frame(d, index, &src);
+  if (rc != SDF_OK) return rc;
+  const size_t n = (size_t)d->W * d->H * (size_t)sdf_format_bytes(d->format);
+  if (!dst || bytes < (int64_t)n) return SDF_E_INVALID_ARG;
+  if (hipSetDevice(d->dev) != hipSuccess) return SDF_E_HIP;
+  // after everything queued for the frame's buffer set (render, decode)
+  const int b = (int)(index % d->nbuf);
+  hipEvent_t e = nullptr;
+  rc = hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (rc == SDF_OK) rc = hip_ok(hipEventRecord(e, d->rs[b]));
+  if (rc == SDF_OK) rc = hip_ok(hipStreamWaitEvent((hipStream_t)stream, e, 0));
+  if (rc == SDF_OK)
+    rc = hip_ok(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  if (e) (void)hipEventDestroy(e);
+  return rc;
+}
+
+int sdf_driver_destroy(sdf_driver* d) {
+  if (!d) return SDF_OK;
+  int rc = SDF_OK;
+  if (d->error == SDF_OK) rc = sdf_driver_drain(d);
+  release(d);
+  return rc;
+}
+
+}  // extern "C"

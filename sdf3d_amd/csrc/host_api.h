@@ -1,0 +1,40 @@
+// host_api.h -- library-internal host interfaces shared by the C-ABI
+// (sdf_abi.cpp) and the native frame driver (driver.cpp).  Not installed.
+#pragma once
+
+#include "../../include/sdf_abi.h"
+#include "kernel_args.h"
+
+namespace sdf {
+
+// One validated, prepared render launch: the kernel arguments of an
+// sdf_render call (camera hoisted, primitive blocks and culling bounds
+// prepared) plus the kernel that serves it.  Building one costs a few
+// microseconds of host time; launching one is the kernel launch alone
+// (plus the TILES compaction).  sdf_render builds and launches one per call;
+// the frame driver keeps one per buffer set and re-launches it every frame.
+struct RenderPlan {
+  KernelArgs a;
+  int variant;             // built-in variant, or kVariantGeneric
+  bool jit;                // a run-time specialised kernel is tried first
+  bool exact;
+  int sig[SDF_MAX_PRIMS];  // the scene signature (jit)
+  int nsig;
+  int rows;                // 0: nothing to render
+  int tiles_ntiles;        // > 0: TILES output, compacted after the render
+};
+
+// Rows a tiling owns (sdf_owned_rows), or SDF_E_INVALID_ARG.
+int count_rows(int height, const sdf_tiling& t);
+int tiling_run(const sdf_tiling& t);
+
+// Validate and prepare (tiling NULL = the whole frame).  SDF_OK or an SDF_E_*.
+int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                     const sdf_material* material, const sdf_params* params,
+                     const sdf_tiling* tiling, void* rgba, int32_t* steps, RenderPlan* plan);
+// Replace the camera of a prepared plan (validated by the caller).
+void plan_set_camera(RenderPlan* plan, const sdf_camera* camera);
+// Enqueue a prepared plan on `stream`.  SDF_OK or SDF_E_HIP.
+int launch_render_plan(const RenderPlan& plan, void* stream);
+
+}  // namespace sdf

@@ -15,6 +15,7 @@
 #include <initializer_list>
 
 #include "../../include/sdf_abi.h"
+#include "host_api.h"
 #include "kernel_args.h"
 
 // Layout contract with the ctypes mirror (sdf3d_amd/abi.py STRUCT_SIZES).
@@ -25,6 +26,26 @@ static_assert(sizeof(sdf_light) == 32, "sdf_light layout");
 static_assert(sizeof(sdf_material) == 40, "sdf_material layout");
 static_assert(sizeof(sdf_params) == 80, "sdf_params layout");
 static_assert(sizeof(sdf_tiling) == 20, "sdf_tiling layout");
+static_assert(sizeof(sdf_driver_config) == 32, "sdf_driver_config layout");
+
+namespace sdf {
+
+int tiling_run(const sdf_tiling& t) { return t.block_run > 1 ? t.block_run : 1; }
+
+int count_rows(int height, const sdf_tiling& t) {
+  if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0 ||
+      t.block_run < 0 || tiling_run(t) > t.block_stride ||
+      (t.flags & ~SDF_TILING_FRAME_ROWS) != 0)
+    return SDF_E_INVALID_ARG;
+  // every period contributes its run of blocks, cut at the frame's last row
+  long long rows = 0;
+  const long long B = t.block_rows;
+  for (long long b = t.first_block; b * B < height; b += t.block_stride)
+    rows += std::min<long long>((b + tiling_run(t)) * B, height) - b * B;
+  return (int)rows;
+}
+
+}  // namespace sdf
 
 namespace {
 
@@ -76,19 +97,8 @@ bool finite3(const float* v) {
   return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]);
 }
 
-int run_of(const sdf_tiling& t) { return t.block_run > 1 ? t.block_run : 1; }
-
-int count_rows(int height, const sdf_tiling& t) {
-  if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0 ||
-      t.block_run < 0 || run_of(t) > t.block_stride || (t.flags & ~SDF_TILING_FRAME_ROWS) != 0)
-    return SDF_E_INVALID_ARG;
-  // every period contributes its run of blocks, cut at the frame's last row
-  long long rows = 0;
-  const long long B = t.block_rows;
-  for (long long b = t.first_block; b * B < height; b += t.block_stride)
-    rows += std::min<long long>((b + run_of(t)) * B, height) - b * B;
-  return (int)rows;
-}
+int run_of(const sdf_tiling& t) { return sdf::tiling_run(t); }
+using sdf::count_rows;
 
 const sdf_tiling kWholeFrame = {8, 0, 1, 0, 1};
 
@@ -221,6 +231,118 @@ int select_variant(const sdf_scene& scene) {
   SDF_FIXED_VARIANTS(SDF_MATCH)
 #undef SDF_MATCH
   return kVariantGeneric;
+}
+
+}  // namespace sdf
+
+namespace sdf {
+
+void plan_set_camera(RenderPlan* plan, const sdf_camera* camera) {
+  KernelArgs& a = plan->a;
+  invert_view(camera->view, a.inv_view);
+  const float* m = a.inv_view;
+  // :180 camera.pos = (inverse(V_mat) * vec4(camera.pos, 1)).xyz, fp32
+  for (int i = 0; i < 3; ++i)
+    a.cam[i] = m[i] * camera->eye[0] + m[4 + i] * camera->eye[1] + m[8 + i] * camera->eye[2] +
+               m[12 + i] * 1.0f;
+  // :191 -2.0f / tan(camera.fov * PI / 360.0f), fp32
+  const float ang = camera->fov_deg * camera->pi / 360.0f;
+  a.focal = -2.0f / tanf(ang);
+  a.aspect = camera->aspect > 0.0f ? camera->aspect : (float)a.width / (float)a.height;
+}
+
+int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                     const sdf_material* material, const sdf_params* params,
+                     const sdf_tiling* tiling, void* rgba, int32_t* steps, RenderPlan* plan) {
+  int rc = sdf_validate(scene, camera, light, material, params, tiling);
+  if (rc != SDF_OK) return rc;
+  if (!plan) return SDF_E_INVALID_ARG;
+  const sdf_tiling t = tiling ? *tiling : kWholeFrame;
+  const int rows = count_rows(params->height, t);
+  std::memset(plan, 0, sizeof(*plan));
+  plan->rows = rows;
+  if (rows == 0) return SDF_OK;  // a rank that owns no block: nothing to write
+  if (!rgba) return SDF_E_INVALID_ARG;
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SDF_E_NO_DEVICE;
+
+  KernelArgs& a = plan->a;
+  a.width = params->width;
+  a.height = params->height;
+  plan_set_camera(plan, camera);
+  for (int i = 0; i < 3; ++i) {
+    a.light_pos[i] = light->pos[i];
+    a.mat_amb[i] = material->amb[i];
+    a.mat_dif[i] = material->dif[i];
+    a.mat_ref[i] = material->ref[i];
+  }
+  a.light_amb = light->ambient;
+  a.shininess = material->shininess;
+  a.max_steps = params->max_steps;
+  a.max_dist = params->max_dist;
+  a.eps = params->eps;
+  a.shadow_k = params->shadow_k;
+  a.normal_eps = params->normal_eps;
+  a.shadow_offset = params->shadow_offset;
+  a.flags = params->flags;
+  a.normal_mode = params->normal_mode;
+  a.format = params->output_format;
+  a.ao_taps = (params->flags & SDF_FLAG_AO) ? params->ao_taps : 0;
+  a.ao_step = params->ao_step;
+  a.ao_base = params->ao_base;
+  a.ao_falloff = params->ao_falloff;
+  a.ao_strength = params->ao_strength;
+  // AO tap heights, in the oracle's fp32 operation order (oracle_core.h
+  // ambient_occlusion): t = i / (taps - 1); h = base + step * t
+  for (int i = 0; i < a.ao_taps && i < kMaxAoTaps; ++i) {
+    const float tt = a.ao_taps > 1 ? (float)i / (float)(a.ao_taps - 1) : 0.0f;
+    a.ao_h[i] = params->ao_base + params->ao_step * tt;
+  }
+  a.inv_width = 1.0f / (float)params->width;
+  a.inv_height = 1.0f / (float)params->height;
+  a.block_rows = t.block_rows;
+  a.chunk_rows = t.block_rows * run_of(t);
+  a.first_block = t.first_block;
+  a.block_stride = t.block_stride;
+  a.rows = rows;
+  a.frame_rows = (t.flags & SDF_TILING_FRAME_ROWS) ? 1 : 0;
+  a.scene_kind = scene->kind;
+  a.prim_count = scene->kind == SDF_SCENE_PRIMITIVES ? scene->count : 0;
+  for (int i = 0; i < 3; ++i) a.bulb_center[i] = scene->bulb_center[i];
+  a.bulb_scale = scene->bulb_scale;
+  a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
+  a.bulb_iterations = scene->bulb_iterations;
+  prepare_prims(*scene, a.prims);
+  if (scene->kind == SDF_SCENE_PRIMITIVES) prepare_bounds(*scene, a);
+  a.bulb_inv_scale = 1.0f / scene->bulb_scale;
+  a.rgba = rgba;
+  a.steps = steps;
+
+  const bool generic = params->dispatch != SDF_DISPATCH_AUTO &&
+                       scene->kind == SDF_SCENE_PRIMITIVES;
+  if (params->dispatch == SDF_DISPATCH_UNCULLED) a.cluster_first = a.prim_count;
+  plan->variant = generic ? kVariantGeneric : select_variant(*scene);
+  plan->exact = params->precision == SDF_PRECISION_EXACT;
+  // no built-in specialisation: a run-time compiled one (jit.cpp)
+  plan->jit = plan->variant == kVariantGeneric && !generic && a.prim_count > 0;
+  if (plan->jit) plan->nsig = scene_signature(*scene, plan->sig);
+  plan->tiles_ntiles = params->output_format == SDF_FORMAT_TILES
+                           ? ((params->width + 7) / 8) * ((rows + 7) / 8)
+                           : 0;
+  return SDF_OK;
+}
+
+int launch_render_plan(const RenderPlan& plan, void* stream) {
+  if (plan.rows == 0) return SDF_OK;
+  int err = -1;
+  if (plan.jit) err = launch_render_jit(plan.a, plan.sig, plan.nsig, plan.exact, stream);
+  if (err == -1)
+    err = plan.exact ? launch_render_exact(plan.a, plan.variant, stream)
+                     : launch_render_fast(plan.a, plan.variant, stream);
+  if (err == hipSuccess && plan.tiles_ntiles > 0)
+    err = launch_tiles_compact(plan.a.rgba, plan.tiles_ntiles, stream);
+  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 
 }  // namespace sdf
@@ -377,96 +499,11 @@ int64_t sdf_tiles_bytes(int32_t width, int32_t rows) {
 int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
                const sdf_material* material, const sdf_params* params,
                const sdf_tiling* tiling, void* rgba, int32_t* steps, void* stream) {
-  int rc = sdf_validate(scene, camera, light, material, params, tiling);
+  sdf::RenderPlan plan;
+  const int rc = sdf::make_render_plan(scene, camera, light, material, params, tiling, rgba,
+                                       steps, &plan);
   if (rc != SDF_OK) return rc;
-  const sdf_tiling t = tiling ? *tiling : kWholeFrame;
-  const int rows = count_rows(params->height, t);
-  if (rows == 0) return SDF_OK;  // a rank that owns no block: nothing to write
-  if (!rgba) return SDF_E_INVALID_ARG;
-
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SDF_E_NO_DEVICE;
-
-  sdf::KernelArgs a;
-  std::memset(&a, 0, sizeof(a));
-  invert_view(camera->view, a.inv_view);
-  const float* m = a.inv_view;
-  // :180 camera.pos = (inverse(V_mat) * vec4(camera.pos, 1)).xyz, fp32
-  for (int i = 0; i < 3; ++i)
-    a.cam[i] = m[i] * camera->eye[0] + m[4 + i] * camera->eye[1] + m[8 + i] * camera->eye[2] +
-               m[12 + i] * 1.0f;
-  // :191 -2.0f / tan(camera.fov * PI / 360.0f), fp32
-  const float ang = camera->fov_deg * camera->pi / 360.0f;
-  a.focal = -2.0f / tanf(ang);
-  a.aspect = camera->aspect > 0.0f ? camera->aspect
-                                   : (float)params->width / (float)params->height;
-  for (int i = 0; i < 3; ++i) {
-    a.light_pos[i] = light->pos[i];
-    a.mat_amb[i] = material->amb[i];
-    a.mat_dif[i] = material->dif[i];
-    a.mat_ref[i] = material->ref[i];
-  }
-  a.light_amb = light->ambient;
-  a.shininess = material->shininess;
-  a.width = params->width;
-  a.height = params->height;
-  a.max_steps = params->max_steps;
-  a.max_dist = params->max_dist;
-  a.eps = params->eps;
-  a.shadow_k = params->shadow_k;
-  a.normal_eps = params->normal_eps;
-  a.shadow_offset = params->shadow_offset;
-  a.flags = params->flags;
-  a.normal_mode = params->normal_mode;
-  a.format = params->output_format;
-  a.ao_taps = (params->flags & SDF_FLAG_AO) ? params->ao_taps : 0;
-  a.ao_step = params->ao_step;
-  a.ao_base = params->ao_base;
-  a.ao_falloff = params->ao_falloff;
-  a.ao_strength = params->ao_strength;
-  // AO tap heights, in the oracle's fp32 operation order (oracle_core.h
-  // ambient_occlusion): t = i / (taps - 1); h = base + step * t
-  for (int i = 0; i < a.ao_taps && i < sdf::kMaxAoTaps; ++i) {
-    const float t = a.ao_taps > 1 ? (float)i / (float)(a.ao_taps - 1) : 0.0f;
-    a.ao_h[i] = params->ao_base + params->ao_step * t;
-  }
-  a.inv_width = 1.0f / (float)params->width;
-  a.inv_height = 1.0f / (float)params->height;
-  a.block_rows = t.block_rows;
-  a.chunk_rows = t.block_rows * run_of(t);
-  a.first_block = t.first_block;
-  a.block_stride = t.block_stride;
-  a.rows = rows;
-  a.frame_rows = (t.flags & SDF_TILING_FRAME_ROWS) ? 1 : 0;
-  a.scene_kind = scene->kind;
-  a.prim_count = scene->kind == SDF_SCENE_PRIMITIVES ? scene->count : 0;
-  for (int i = 0; i < 3; ++i) a.bulb_center[i] = scene->bulb_center[i];
-  a.bulb_scale = scene->bulb_scale;
-  a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
-  a.bulb_iterations = scene->bulb_iterations;
-  prepare_prims(*scene, a.prims);
-  if (scene->kind == SDF_SCENE_PRIMITIVES) prepare_bounds(*scene, a);
-  a.bulb_inv_scale = 1.0f / scene->bulb_scale;
-  a.rgba = rgba;
-  a.steps = steps;
-
-  const bool generic = params->dispatch != SDF_DISPATCH_AUTO &&
-                       scene->kind == SDF_SCENE_PRIMITIVES;
-  if (params->dispatch == SDF_DISPATCH_UNCULLED) a.cluster_first = a.prim_count;
-  const int variant = generic ? sdf::kVariantGeneric : sdf::select_variant(*scene);
-  int err = -1;
-  if (variant == sdf::kVariantGeneric && !generic && a.prim_count > 0) {
-    // no built-in specialisation: a run-time compiled one (jit.cpp)
-    int sig[SDF_MAX_PRIMS];
-    const int n = sdf::scene_signature(*scene, sig);
-    err = sdf::launch_render_jit(a, sig, n, params->precision == SDF_PRECISION_EXACT, stream);
-  }
-  if (err == -1)
-    err = params->precision == SDF_PRECISION_FAST ? sdf::launch_render_fast(a, variant, stream)
-                                                  : sdf::launch_render_exact(a, variant, stream);
-  if (err == hipSuccess && params->output_format == SDF_FORMAT_TILES)
-    err = sdf::launch_tiles_compact(rgba, ((params->width + 7) / 8) * ((rows + 7) / 8), stream);
-  return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+  return sdf::launch_render_plan(plan, stream);
 }
 
 int sdf_jit_count(void) { return sdf::jit_compiled_count(); }
@@ -545,6 +582,8 @@ const char* sdf_strerror(int code) {
     case SDF_E_UNSUPPORTED: return "unsupported request";
     case SDF_E_HIP: return "HIP runtime error";
     case SDF_E_NO_DEVICE: return "no HIP device available";
+    case SDF_E_COMM: return "RCCL unavailable or a collective failed";
+    case SDF_E_TIMEOUT: return "frame driver wait timed out";
     default: return "unknown error";
   }
 }

@@ -1,0 +1,145 @@
+"""Python handle on the native multi-device frame driver (include/sdf_abi.h
+``sdf_comm_*`` / ``sdf_driver_*``, sdf3d_amd/csrc/driver.cpp).
+
+One process per GPU, as launched by torchrun.  torch.distributed is used
+once, to hand every rank the RCCL unique ids of the driver's two
+communicators; from then on every per-frame call is one ctypes call into
+the library, which renders, agrees the TILES stream lengths (RCCL
+all-gather), ships the streams to rank 0 (RCCL send/recv) and decodes them
+there -- the same sequence as ``multigpu.FrameDriver`` (whose gloo
+rehearsal in tests/test_multigpu_cpu.py pins the collective order) at a
+fraction of its host cost (tools/driver_probe.py).  The driver loads the
+RCCL library this process already has mapped (PyTorch's), so one RCCL
+instance serves both.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import abi
+from .scenes import Frame
+
+
+def loaded_rccl_path() -> str:
+    """Path of the librccl this process has mapped (PyTorch loads one with
+    its HIP backend), else PyTorch's bundled one, else the system's."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.rsplit(None, 1)[-1] if "/" in line else ""
+                if "librccl" in os.path.basename(path):
+                    return path
+    except OSError:  # pragma: no cover - non-Linux
+        pass
+    try:
+        import torch
+        p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        if os.path.exists(p):
+            return p
+    except ImportError:  # pragma: no cover
+        pass
+    return "librccl.so.1"
+
+
+class Comm:
+    """One RCCL communicator over the torch.distributed world (collective:
+    every rank constructs it, in the same order)."""
+
+    def __init__(self, dist, device, rccl_path: str | None = None):
+        import torch
+        self.lib = abi.load_library()
+        self.path = (rccl_path or loaded_rccl_path()).encode()
+        rank, world = dist.get_rank(), dist.get_world_size()
+        uid = torch.zeros(abi.COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            buf = (C.c_uint8 * abi.COMM_ID_BYTES)()
+            abi.check(self.lib.sdf_comm_unique_id(self.path, buf), "sdf_comm_unique_id")
+            uid = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8)
+        on_dev = dist.get_backend() == "nccl"
+        t = uid.to(device) if on_dev else uid
+        dist.broadcast(t, src=0)
+        raw = bytes(t.cpu().numpy().tobytes())
+        self.handle = C.c_void_p()
+        with torch.cuda.device(device):
+            abi.check(self.lib.sdf_comm_create(self.path, raw, world, rank,
+                                               C.byref(self.handle)), "sdf_comm_create")
+
+    def close(self):
+        if self.handle:
+            self.lib.sdf_comm_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+
+class NativeFrameDriver:
+    """The frame loop in C++ (sdf_driver_*).  ``step()`` enqueues one frame;
+    ``drain()`` ships everything and waits; ``read_frame(i, out)`` copies
+    rank 0's frame i (one of the last ``nbuf``) into a torch tensor."""
+
+    def __init__(self, frame: Frame, rank: int, world: int, device, shares=(1, 1), nbuf: int = 4,
+                 lag: int = 2, dist=None, root_as_peer: bool = False, timeout_ms: int = 60000):
+        import torch
+        self.torch = torch
+        self.lib = abi.load_library()
+        self.device = torch.device(device)
+        self.frame_desc = frame
+        self.rank, self.world, self.nbuf = rank, world, nbuf
+        self.comms = []
+        cfg = abi.sdf_driver_config(rank=rank, world=world, share_root=shares[0],
+                                    share_peer=shares[1], nbuf=nbuf, lag=lag,
+                                    flags=abi.DRIVER_ROOT_AS_PEER if root_as_peer else 0,
+                                    timeout_ms=timeout_ms)
+        if world > 1 or root_as_peer:
+            if dist is None:
+                raise ValueError("a multi-rank driver needs torch.distributed for its comm ids")
+            self.comms = [Comm(dist, self.device), Comm(dist, self.device)]
+        self.handle = C.c_void_p()
+        sc = [c.handle for c in self.comms] or [None, None]
+        with torch.cuda.device(self.device):
+            abi.check(self.lib.sdf_driver_create(
+                C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
+                C.byref(frame.material), C.byref(frame.params), C.byref(cfg), sc[0], sc[1],
+                C.byref(self.handle)), "sdf_driver_create")
+        self._idx = C.c_int64()
+
+    def step(self) -> int:
+        rc = self.lib.sdf_driver_step(self.handle, C.byref(self._idx))
+        if rc != abi.SDF_OK:
+            abi.check(rc, "sdf_driver_step")
+        return self._idx.value
+
+    def set_camera(self, camera) -> None:
+        abi.check(self.lib.sdf_driver_set_camera(self.handle, C.byref(camera)),
+                  "sdf_driver_set_camera")
+
+    def drain(self) -> None:
+        abi.check(self.lib.sdf_driver_drain(self.handle), "sdf_driver_drain")
+
+    def read_frame(self, index: int, out=None, stream=None):
+        """Rank 0's frame `index` as a (H, W, 4) tensor of the frame format."""
+        from .renderer import channels, torch_dtype
+        torch = self.torch
+        p = self.frame_desc.params
+        if out is None:
+            out = torch.empty((p.height, p.width, channels(p.output_format)),
+                              dtype=torch_dtype(p.output_format), device=self.device)
+        s = stream or torch.cuda.current_stream(self.device)
+        abi.check(self.lib.sdf_driver_read_frame(
+            self.handle, index, C.c_void_p(out.data_ptr()),
+            out.numel() * out.element_size(), C.c_void_p(s.cuda_stream)), "sdf_driver_read_frame")
+        return out
+
+    def close(self) -> None:
+        if self.handle:
+            rc = self.lib.sdf_driver_destroy(self.handle)
+            self.handle = C.c_void_p()
+            for c in self.comms:
+                c.close()
+            self.comms = []
+            abi.check(rc, "sdf_driver_destroy")
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -24,17 +24,22 @@ Collective streams: the TILES size agreement has a process group of its
 own (its own RCCL communicator and stream) so it never queues behind a
 gather.
 
-Pipelining: nbuf (3) buffer sets and one render stream per set, so frame
+Pipelining: nbuf buffer sets and one render stream per set, so frame
 i+1 starts while frame i's slowest tiles finish (a launch of one rank's
 share ends with its slowest 8x8 tile: ~0.11 ms for 1/8 of the 4K frame on
 one stream, ~0.05 ms per frame on alternating streams) and while frame i is
 gathered (RCCL) and assembled on rank 0 (TILES: on frame i's own render
-stream; raw rows: on a side stream).  In "tiles" mode
-the gather of frame i is issued after frame i+1's render, once frame i's
-size is known; every collective is issued in an order that keeps the single
-RCCL stream from holding one frame's transfer behind the next one's render.
-A buffer is reused only after the collective (and on rank 0 the assembly)
-that read it has finished.
+stream; raw rows: on a side stream).  In "tiles" mode the gather of frame i
+is issued `lag` steps later (after frame i + lag's render is enqueued), once
+frame i's agreed size has reached the host: the agreed size is copied into
+pinned host memory on the frame's stream and read after an event wait, so
+with lag >= 2 the host finds it there without stalling and always keeps
+frames queued ahead of the GPU (with lag 1 it waits for the frame just
+rendered while only one frame is queued).  Every collective is issued in
+the same order on all ranks, in an order that keeps the single RCCL stream
+from holding one frame's transfer behind the next one's render.  A buffer
+is reused only after the collective (and on rank 0 the assembly) that read
+it has finished: lag <= nbuf - 1.
 
 The render and assembly steps are injected, so the same driver runs the HIP
 kernels on GPUs (bench.py) and CPU stand-ins under the gloo backend
@@ -129,7 +134,10 @@ class FrameDriver:
                  render_fn: Callable, deinterleave_fn: Callable, block_rows: int = 8,
                  nbuf: int = 3, dist=None, dtype=None, wire_channels: int = 4,
                  wire: str = "raw", wire_bytes: Optional[int] = None,
-                 root_render_fn: Optional[Callable] = None, shares=(1, 1)):
+                 root_render_fn: Optional[Callable] = None, shares=(1, 1),
+                 lag: int = 2, collectives_at_world1: bool = False):
+        import collections
+
         import torch
         self.torch = torch
         self.W, self.H = width, height
@@ -155,7 +163,13 @@ class FrameDriver:
                           for r in range(world))
         self.gpu = getattr(device, "type", str(device)).startswith("cuda")
         self.nbuf = nbuf
-        self.wire = wire if world > 1 else "raw"
+        # collectives_at_world1: run the N > 1 code path with one rank (host
+        # cost probes of the collectives, tools/driver_probe.py)
+        self.multi = world > 1 or collectives_at_world1
+        self.wire = wire if self.multi else "raw"
+        self.lag = lag
+        if self.wire == "tiles" and not 1 <= lag <= nbuf - 1:
+            raise ValueError(f"lag must be in [1, nbuf - 1] (nbuf {nbuf}), got {lag}")
         self.root = rank == 0
         self.works = [None] * nbuf
         if self.wire == "tiles":
@@ -169,7 +183,12 @@ class FrameDriver:
             self.local = [torch.zeros((self.cap,), dtype=torch.uint8, device=device)
                           for _ in range(nbuf)]
             self.size_works = [None] * nbuf
-            self.pending = None                       # (i, b) rendered, not yet shipped
+            self.pending = collections.deque()        # (i, b) rendered, not yet shipped
+            if self.gpu:
+                # agreed sizes land here (pinned: an async copy on the frame's
+                # stream, read after its event)
+                self.size_host = torch.zeros((nbuf,), dtype=torch.int32, pin_memory=True)
+                self.size_ev = [torch.cuda.Event() for _ in range(nbuf)]
             # the size agreement runs in its own process group: its own RCCL
             # communicator and stream, so frame i's all-reduce completes
             # while frame i-1's gather is still on the links, and the
@@ -183,17 +202,17 @@ class FrameDriver:
             dtype = dtype or torch.float32   # the framebuffer format on the wire
             mk = lambda *shape: torch.empty(shape, dtype=dtype, device=device)  # noqa: E731
             wc = wire_channels   # 3: RGB32F wire, alpha restored by the deinterleave
-            self.local = [mk(self.stride, width, wc if world > 1 else 4) for _ in range(nbuf)]
-            if world > 1 and self.root:
+            self.local = [mk(self.stride, width, wc if self.multi else 4) for _ in range(nbuf)]
+            if self.multi and self.root:
                 self.gathered = [mk(world * self.stride, width, wc) for _ in range(nbuf)]
-        if world > 1 and self.root:
+        if self.multi and self.root:
             self.frames = [torch.empty((height, width, 4), dtype=torch.float32 if self.wire ==
                                        "tiles" else (dtype or torch.float32), device=device)
                            for _ in range(nbuf)]
             self.asm_done = [None] * nbuf
         if self.gpu:
             self.streams = [torch.cuda.Stream(device=device) for _ in range(nbuf)]
-            self.side = torch.cuda.Stream(device=device) if world > 1 else None
+            self.side = torch.cuda.Stream(device=device) if self.multi else None
         else:
             self.streams = [None] * nbuf
             self.side = None
@@ -214,7 +233,7 @@ class FrameDriver:
             if not self.gpu and self.root and self.wire == "raw":
                 self._cpu_finish(b)
         out = self.local[b] if self.wire == "tiles" else self.local[b][:self.rows]
-        if self.world == 1:
+        if not self.multi:
             # no collectives: the stream goes to the calls explicitly (a
             # stream context costs more host time than a small frame renders)
             if ev_before is not None:
@@ -267,14 +286,18 @@ class FrameDriver:
     # ---- TILES streams -------------------------------------------------------
     def _step_tiles(self, i, b, s):
         import torch.distributed as tdist
-        if self.pending is not None:
-            self._ship(*self.pending)
+        if len(self.pending) >= self.lag:
+            self._ship(*self.pending.popleft())
         with self._ctx(s):
             # the ranks agree on the largest `used` (header word 0, reduced in
             # place: the decoder reads only the offset table and the heads)
             self.size_works[b] = self.dist.all_reduce(self._used(b), op=tdist.ReduceOp.MAX,
                                                       group=self.size_group, async_op=True)
-        self.pending = (i, b)
+            if self.gpu:
+                self.size_works[b].wait()          # stream s waits for the reduction
+                self.size_host[b:b + 1].copy_(self._used(b), non_blocking=True)
+                self.size_ev[b].record(s)
+        self.pending.append((i, b))
 
     def _used(self, b):
         return self.local[b][:4].view(self.torch.int32)
@@ -284,9 +307,14 @@ class FrameDriver:
         torch, dist = self.torch, self.dist
         s = self.streams[b]
         with self._ctx(s):
-            self.size_works[b].wait()
-            # host sync: frame i rendered (and its size reduced) everywhere
-            count = self.data_off + int(self._used(b).item())
+            # host wait: frame i rendered (and its size reduced) everywhere
+            if self.gpu:
+                self.size_ev[b].synchronize()
+                used = int(self.size_host[b])
+            else:
+                self.size_works[b].wait()
+                used = int(self._used(b).item())
+            count = self.data_off + used
             self.size_works[b] = None
             if self.root:
                 # the decode of frame i - nbuf, which read gathered[b], is
@@ -316,14 +344,13 @@ class FrameDriver:
                                      self.B, self.frames[b], None, shares=self.shares)
 
     def drain(self) -> None:
-        if self.wire == "tiles" and self.pending is not None:
-            self._ship(*self.pending)
-            self.pending = None
+        while self.wire == "tiles" and self.pending:
+            self._ship(*self.pending.popleft())
         for b, w in enumerate(self.works):
             if w is not None:
                 w.wait()
                 self.works[b] = None
-                if not self.gpu and self.root and self.world > 1 and self.wire == "raw":
+                if not self.gpu and self.root and self.multi and self.wire == "raw":
                     self._cpu_finish(b)
         if self.gpu:
             self.torch.cuda.synchronize(self.device)
@@ -331,7 +358,7 @@ class FrameDriver:
     def frame(self, i: int):
         """Rank 0's assembled frame of step i (valid after drain(); the last
         nbuf frames are kept)."""
-        if self.world == 1:
+        if not self.multi:
             return self.local[i % self.nbuf][:self.H]
         if not self.root:
             return None

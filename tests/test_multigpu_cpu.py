@@ -41,7 +41,7 @@ def tiles_decode_cpu(parts, world, cap, W, H, B, out, stream=None, shares=(1, 1)
     return out
 
 
-def _worker(rank, world, port, q, wire_channels=4, direct=False, shares=(1, 1)):
+def _worker(rank, world, port, q, wire_channels=4, direct=False, shares=(1, 1), lag=2, nbuf=3):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -70,21 +70,20 @@ def _worker(rank, world, port, q, wire_channels=4, direct=False, shares=(1, 1)):
             drv = FrameDriver(W, H, rank, world, torch.device("cpu"), render_fn,
                               tiles_decode_cpu, dist=dist, wire="tiles",
                               wire_bytes=tiles_ref.capacity(W, big),
-                              root_render_fn=root_fn if direct else None, shares=shares)
+                              root_render_fn=root_fn if direct else None, shares=shares,
+                              lag=lag, nbuf=nbuf)
         else:
             drv = FrameDriver(W, H, rank, world, torch.device("cpu"),
                               render_fn, deinterleave_torch, dist=dist,
                               wire_channels=wire_channels)
         frames = []
-        for i in range(5):
+        for i in range(6):
             step_box[0] = i
             drv.step(i)
-            if i >= 1 and rank == 0:
-                pass
         drv.drain()
         if rank == 0:
             # buffers hold the last nbuf frames
-            for i in (2, 3, 4):
+            for i in range(6 - nbuf, 6):
                 frames.append((i, drv.frame(i).clone().numpy()))
             q.put(frames)
         dist.barrier()
@@ -92,19 +91,21 @@ def _worker(rank, world, port, q, wire_channels=4, direct=False, shares=(1, 1)):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,wire,direct,shares", [
-    (2, 4, False, (1, 1)), (3, 4, False, (1, 1)), (2, 3, False, (1, 1)),
-    (2, "tiles", False, (1, 1)), (3, "tiles", True, (1, 1)), (3, "tiles", True, (1, 2)),
-    (4, "tiles", False, (2, 3))])
-def test_frame_driver_gloo(world, wire, direct, shares):
+@pytest.mark.parametrize("world,wire,direct,shares,lag,nbuf", [
+    (2, 4, False, (1, 1), 2, 3), (3, 4, False, (1, 1), 2, 3), (2, 3, False, (1, 1), 2, 3),
+    (2, "tiles", False, (1, 1), 2, 3), (3, "tiles", True, (1, 1), 2, 3),
+    (3, "tiles", True, (1, 2), 2, 4), (4, "tiles", False, (2, 3), 2, 3),
+    (2, "tiles", True, (1, 1), 1, 3), (3, "tiles", True, (1, 2), 3, 4)])
+def test_frame_driver_gloo(world, wire, direct, shares, lag, nbuf):
     """wire = 3: the lossless RGB32F wire format (alpha restored on rank 0);
     "tiles": the compressed TILES streams (NumPy codec standing in for the
-    kernels), variable-length, with the per-frame size agreement; shares:
-    unequal row shares (rank 0 fewer)."""
+    kernels), variable-length, with the per-frame size agreement, shipped
+    `lag` steps after the render over `nbuf` buffer sets; shares: unequal
+    row shares (rank 0 fewer)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire, direct, shares))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire, direct, shares, lag, nbuf))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -157,3 +158,10 @@ def test_index_math_matches_c_abi(H, world):
     for r in range(world):
         ids = owned_row_ids(H, r, world)
         assert np.array_equal(idx[ids], r * stride + np.arange(len(ids)))
+
+
+def test_lag_bound():
+    """A buffer set is reused after nbuf steps: it must have been shipped by then."""
+    with pytest.raises(ValueError):
+        FrameDriver(16, 16, 0, 1, torch.device("cpu"), None, None, wire="tiles", nbuf=3, lag=3,
+                    collectives_at_world1=True, wire_bytes=4096)
