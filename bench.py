@@ -78,6 +78,9 @@ def parse():
                     help="frame loop: native = sdf_driver_* (C++, RCCL called directly); "
                          "python = multigpu.FrameDriver over torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--clock-warm-s", type=float, default=0.3,
+                    help="seconds of render launches before anything is measured (the "
+                         "GPU's clocks ramp up over ~0.1 s of load)")
     ap.add_argument("--cpu-sample-stride", type=int, default=4,
                     help="CPU baseline renders every k-th 8-row block of the frame")
     ap.add_argument("--cpu-frames", type=int, default=5)
@@ -309,6 +312,34 @@ def main():
             el = float(e.item())
         return el, [e0[i].elapsed_time(e1[i]) for i in range(warmup, k)], drv
 
+    # the render kernel's own launch duration, for the roofline: the rank's
+    # rows as RGBA32F, launches serialised on one stream with events around
+    # each (in the pipelined frame loop a launch's events would also span
+    # time queued behind the other streams' kernels).  Measured before the
+    # frame loop, which it also brings out of the GPU's idle clocks.
+    fk = frame.copy()
+    fk.params.output_format = abi.FORMAT_RGBA32F
+    kbuf = rd.alloc(fk, t)[0]
+    ks = torch.cuda.current_stream(dev)
+    # out of the idle clocks first: the GPU takes longer than a few frames to
+    # reach its sustained clock (measured: 50 frames 0.406 ms each, 200 frames
+    # 0.375), so launches run for args.clock_warm_s before any measurement
+    tw = time.perf_counter()
+    while True:
+        for _ in range(10):
+            rd.render(fk, t, out=kbuf, stream=ks)
+        torch.cuda.synchronize(dev)
+        if time.perf_counter() - tw >= args.clock_warm_s:
+            break
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    for a, b in kev:
+        a.record(ks)
+        rd.render(fk, t, out=kbuf, stream=ks)
+        b.record(ks)
+    torch.cuda.synchronize(dev)
+    kavg_ms = sum(a.elapsed_time(b) for a, b in kev) / len(kev)
+    del kbuf
     log(f"[bench] rank {rank}/{world} {args.config} {W}x{H} rows={rows} "
         f"precision={args.precision} warmup={args.warmup} steps={args.steps}")
     elapsed, kernel_ms, drv = timed_run(frame, args.steps, args.warmup)
@@ -366,24 +397,6 @@ def main():
         verified = bool(torch.equal(got.view(torch.uint8), ref.view(torch.uint8)))
         log(f"[bench] assembled frame == single-device frame: {verified}")
 
-    # the render kernel's own launch duration, for the roofline: the rank's
-    # rows as RGBA32F, launches serialised on one stream with events around
-    # each (in the pipelined loop above a launch's events also span time
-    # queued behind the other streams' kernels)
-    fk = frame.copy()
-    fk.params.output_format = abi.FORMAT_RGBA32F
-    kbuf = rd.alloc(fk, t)[0]
-    ks = torch.cuda.current_stream(dev)
-    rd.render(fk, t, out=kbuf, stream=ks)
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    for a, b in kev:
-        a.record(ks)
-        rd.render(fk, t, out=kbuf, stream=ks)
-        b.record(ks)
-    torch.cuda.synchronize(dev)
-    kavg_ms = sum(a.elapsed_time(b) for a, b in kev) / len(kev)
-    del kbuf
     flops = rank_flops(frame, t, args.pose)
 
     native = hasattr(drv, "read_frame")
@@ -418,6 +431,9 @@ def main():
             "display_rgba8": display,
             "no_gather": no_gather,
             "kernel_ms": round(kavg_ms, 4),
+            # host (CPU) time of the frame loop's own calls per frame, waits
+            # for the GPU / peers excluded (native driver only)
+            "driver_host_us_per_frame": drv.stats()["host_us_per_frame"] if native else None,
         }
         if flops is not None:
             ach = flops / (kavg_ms * 1e-3) / 1e12

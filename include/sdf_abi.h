@@ -274,6 +274,13 @@ typedef enum { SDF_TILING_FRAME_ROWS = 1 } sdf_tiling_flags;
 
 /* ---- entry points -------------------------------------------------------- */
 
+/* The packed tiling of `rank`'s share of a `world`-device frame: rank 0
+ * share_root blocks and every other rank share_peer blocks per period of
+ * share_root + share_peer * (world - 1) 8-row blocks (1:1 = plain
+ * interleave; world 1 = the whole frame). */
+int sdf_share_tiling(int32_t rank, int32_t world, int32_t share_root, int32_t share_peer,
+                     sdf_tiling* tiling);
+
 /* ABI version of the loaded library (== SDF_ABI_VERSION when compatible). */
 int sdf_abi_version(void);
 
@@ -364,13 +371,13 @@ int sdf_jit_count(void);
  * render.  Frames rotate over `nbuf` buffer sets, one HIP stream each; frame
  * i is shipped `lag` frames after its render (the host reads its agreed
  * lengths from pinned memory, without stalling the queue when lag >= 2).
- * The collectives run on two communicators (lengths; data), each on its own
- * stream, issued in the same order on every rank.
+ * The RCCL calls go to two communicators, each on a stream of its own (the
+ * lengths; the streams), in the same order on every rank.
  *
  * RCCL is loaded at run time from `rccl_path` (the librccl.so this process
  * already uses, e.g. PyTorch's, so one RCCL instance serves both); the
- * caller exchanges the 128-byte unique id of each communicator (rank 0 makes
- * it with sdf_comm_unique_id) through its own channel.
+ * caller exchanges each communicator's 128-byte unique id (rank 0 makes it
+ * with sdf_comm_unique_id) through its own channel.
  * world == 1 needs no communicator: frames render whole, nothing is shipped. */
 #define SDF_COMM_ID_BYTES 128
 typedef struct sdf_comm sdf_comm;
@@ -397,8 +404,9 @@ typedef struct {
 } sdf_driver_config;
 
 /* The frame format is params->output_format (RGBA32F at world > 1: the wire
- * is lossless TILES).  size_comm / data_comm: two communicators over the
- * same `world` ranks (NULL when world == 1 without ROOT_AS_PEER). */
+ * is lossless TILES).  size_comm, data_comm: two distinct communicators
+ * over the `world` ranks, used by this driver alone (NULL when world == 1
+ * without ROOT_AS_PEER). */
 int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
                       const sdf_material* material, const sdf_params* params,
                       const sdf_driver_config* config, sdf_comm* size_comm, sdf_comm* data_comm,
@@ -418,6 +426,10 @@ int sdf_driver_frame(sdf_driver* driver, int64_t index, void** rgba);
  * all work queued for that frame. */
 int sdf_driver_read_frame(sdf_driver* driver, int64_t index, void* dst, int64_t bytes,
                           void* stream);
+/* Host-time accounting since creation: out[0] frames stepped, out[1]
+ * seconds spent inside sdf_driver_step / sdf_driver_drain, out[2] the part
+ * of out[1] spent waiting for the GPU or a peer (n >= 3). */
+int sdf_driver_stats(sdf_driver* driver, double* out, int32_t n);
 int sdf_driver_destroy(sdf_driver* driver);
 
 /* Short description of a status code. */

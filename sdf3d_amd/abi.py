@@ -114,6 +114,7 @@ SIGNATURES = {
     "sdf_validate": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light), _P(sdf_material),
                                _P(sdf_params), _P(sdf_tiling)]),
     "sdf_owned_rows": (C.c_int, [C.c_int32, _P(sdf_tiling)]),
+    "sdf_share_tiling": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P(sdf_tiling)]),
     "sdf_render": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light), _P(sdf_material),
                              _P(sdf_params), _P(sdf_tiling), C.c_void_p, C.c_void_p, C.c_void_p]),
     "sdf_deinterleave": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
@@ -140,6 +141,7 @@ SIGNATURES = {
     "sdf_driver_frame": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_void_p)]),
     "sdf_driver_read_frame": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                         C.c_void_p]),
+    "sdf_driver_stats": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int32]),
     "sdf_driver_destroy": (C.c_int, [C.c_void_p]),
     "sdf_strerror": (C.c_char_p, [C.c_int]),
 }

@@ -418,6 +418,20 @@ int sdf_defaults(sdf_scene* scene, sdf_camera* camera, sdf_light* light,
   return SDF_OK;
 }
 
+int sdf_share_tiling(int32_t rank, int32_t world, int32_t share_root, int32_t share_peer,
+                     sdf_tiling* tiling) {
+  if (!tiling || world < 1 || rank < 0 || rank >= world || share_root < 1 || share_peer < 1)
+    return SDF_E_INVALID_ARG;
+  const int a = share_root, b = share_peer;
+  if (world == 1) {
+    *tiling = kWholeFrame;
+  } else {
+    *tiling = sdf_tiling{8, rank == 0 ? 0 : a + b * (rank - 1), a + b * (world - 1), 0,
+                         rank == 0 ? a : b};
+  }
+  return SDF_OK;
+}
+
 int sdf_owned_rows(int32_t height, const sdf_tiling* tiling) {
   return count_rows(height, tiling ? *tiling : kWholeFrame);
 }

@@ -3,8 +3,9 @@
 
 One process per GPU, as launched by torchrun.  torch.distributed is used
 once, to hand every rank the RCCL unique ids of the driver's two
-communicators; from then on every per-frame call is one ctypes call into
-the library, which renders, agrees the TILES stream lengths (RCCL
+communicators (stream lengths; stream data, each on its own HIP stream);
+from then on every per-frame call is one ctypes call into the library,
+which renders, agrees the TILES stream lengths (RCCL
 all-gather), ships the streams to rank 0 (RCCL send/recv) and decodes them
 there -- the same sequence as ``multigpu.FrameDriver`` (whose gloo
 rehearsal in tests/test_multigpu_cpu.py pins the collective order) at a
@@ -94,12 +95,14 @@ class NativeFrameDriver:
                 raise ValueError("a multi-rank driver needs torch.distributed for its comm ids")
             self.comms = [Comm(dist, self.device), Comm(dist, self.device)]
         self.handle = C.c_void_p()
-        sc = [c.handle for c in self.comms] or [None, None]
         with torch.cuda.device(self.device):
-            abi.check(self.lib.sdf_driver_create(
+            rc = self.lib.sdf_driver_create(
                 C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
-                C.byref(frame.material), C.byref(frame.params), C.byref(cfg), sc[0], sc[1],
-                C.byref(self.handle)), "sdf_driver_create")
+                C.byref(frame.material), C.byref(frame.params), C.byref(cfg),
+                *([c.handle for c in self.comms] or [None, None]), C.byref(self.handle))
+        if rc != abi.SDF_OK:
+            self._close_comms()
+            abi.check(rc, "sdf_driver_create")
         self._idx = C.c_int64()
 
     def step(self) -> int:
@@ -129,14 +132,26 @@ class NativeFrameDriver:
             out.numel() * out.element_size(), C.c_void_p(s.cuda_stream)), "sdf_driver_read_frame")
         return out
 
+    def stats(self) -> dict:
+        """Host time of the driver's calls: frames, seconds in step/drain, and
+        the seconds of that spent waiting on the GPU or a peer."""
+        out = (C.c_double * 3)()
+        abi.check(self.lib.sdf_driver_stats(self.handle, out, 3), "sdf_driver_stats")
+        n = max(out[0], 1.0)
+        return {"frames": int(out[0]), "call_s": out[1], "wait_s": out[2],
+                "host_us_per_frame": round((out[1] - out[2]) / n * 1e6, 2)}
+
     def close(self) -> None:
         if self.handle:
             rc = self.lib.sdf_driver_destroy(self.handle)
             self.handle = C.c_void_p()
-            for c in self.comms:
-                c.close()
-            self.comms = []
+            self._close_comms()
             abi.check(rc, "sdf_driver_destroy")
+
+    def _close_comms(self) -> None:
+        for c in self.comms:
+            c.close()
+        self.comms = []
 
     def __del__(self):  # pragma: no cover - best effort
         try:

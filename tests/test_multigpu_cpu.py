@@ -132,9 +132,12 @@ def test_share_index_math_matches_c_abi(H, world, shares):
 
 
 def test_choose_shares():
-    from sdf3d_amd.multigpu import choose_shares
+    from sdf3d_amd.multigpu import FRAME_COSTS_MS, choose_shares
     assert choose_shares(1) == (1, 1)
-    assert choose_shares(2) == (1, 1)       # root's decode is cheap next to half a frame
+    a, b = choose_shares(2)
+    assert a >= b                           # the one peer's link is the slower leg
+    no_wire = dict(FRAME_COSTS_MS, wire=0.0)
+    assert choose_shares(2, no_wire) == (1, 1)   # root's decode is cheap next to half a frame
     a, b = choose_shares(8)
     assert a < b                            # rank 0 decodes 7 streams: fewer rows
     # with a free decode the shares balance renders alone
@@ -165,3 +168,23 @@ def test_lag_bound():
     with pytest.raises(ValueError):
         FrameDriver(16, 16, 0, 1, torch.device("cpu"), None, None, wire="tiles", nbuf=3, lag=3,
                     collectives_at_world1=True, wire_bytes=4096)
+
+
+@pytest.mark.parametrize("world,shares", [(1, (1, 1)), (2, (4, 3)), (4, (1, 1)), (8, (1, 2)),
+                                          (5, (3, 2))])
+def test_native_driver_tilings_match(world, shares):
+    """The native driver's shares (sdf_share_tiling) are the Python driver's."""
+    import ctypes as C
+    from sdf3d_amd import abi
+    lib = abi.load_library()
+    for r in range(world):
+        t = abi.sdf_tiling()
+        assert lib.sdf_share_tiling(r, world, shares[0], shares[1], C.byref(t)) == 0
+        want = R.tiling(r, world, 8, shares=shares)
+        for H in (43, 2160):
+            assert R.owned_rows(H, t) == R.owned_rows(H, want) == owned_rows_py(H, r, world, 8, shares)
+        if world > 1:
+            assert (t.block_rows, t.first_block, t.block_stride, t.block_run) == \
+                (want.block_rows, want.first_block, want.block_stride, want.block_run)
+    bad = abi.sdf_tiling()
+    assert lib.sdf_share_tiling(world, world, 1, 1, C.byref(bad)) == abi.SDF_E_INVALID_ARG

@@ -174,8 +174,10 @@ def main():
             drv.step()
         drv.drain()
         el = time.perf_counter() - t0
+        st = drv.stats()
         drv.close()
-        return round(el / frames * 1e3, 4)
+        return {"ms_per_frame": round(el / frames * 1e3, 4),
+                "host_us_per_frame": st["host_us_per_frame"]}
 
     nat = {}
     for lag, nbuf in ((1, 3), (2, 4)):
