@@ -229,6 +229,24 @@ def main():
             open_drivers.append(drv)
         return drv
 
+    fk = frame.copy()
+    fk.params.output_format = abi.FORMAT_RGBA32F
+    kbuf = rd.alloc(fk, t)[0]
+    ks = torch.cuda.current_stream(dev)
+
+    def warm_clocks():
+        """Render launches for args.clock_warm_s seconds: the GPU takes longer
+        than a few frames to leave its idle clocks (measured: 50 frames 0.406
+        ms each, 200 frames 0.375), so every measurement below starts from
+        its sustained clock -- after allocations, which idle it again."""
+        tw = time.perf_counter()
+        while True:
+            for _ in range(10):
+                rd.render(fk, t, out=kbuf, stream=ks)
+            torch.cuda.synchronize(dev)
+            if time.perf_counter() - tw >= args.clock_warm_s:
+                break
+
     def timed_run(fr, steps, warmup):
         """warmup + `steps` timed frames of `fr` through a frame driver; returns
         (max-over-ranks seconds, per-launch kernel ms list, driver)."""
@@ -237,6 +255,7 @@ def main():
                                                                   args.backend == "nccl")
         drv = native_driver(fr) if use_native else None
         if drv is not None:
+            warm_clocks()
             for _ in range(warmup):
                 drv.step()
             drv.drain()
@@ -292,6 +311,7 @@ def main():
         k = steps + warmup
         e0 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
         e1 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        warm_clocks()
         for i in range(warmup):
             drv.step(i, e0[i], e1[i])
         drv.drain()
@@ -315,31 +335,16 @@ def main():
     # the render kernel's own launch duration, for the roofline: the rank's
     # rows as RGBA32F, launches serialised on one stream with events around
     # each (in the pipelined frame loop a launch's events would also span
-    # time queued behind the other streams' kernels).  Measured before the
-    # frame loop, which it also brings out of the GPU's idle clocks.
-    fk = frame.copy()
-    fk.params.output_format = abi.FORMAT_RGBA32F
-    kbuf = rd.alloc(fk, t)[0]
-    ks = torch.cuda.current_stream(dev)
-    # out of the idle clocks first: the GPU takes longer than a few frames to
-    # reach its sustained clock (measured: 50 frames 0.406 ms each, 200 frames
-    # 0.375), so launches run for args.clock_warm_s before any measurement
-    tw = time.perf_counter()
-    while True:
-        for _ in range(10):
-            rd.render(fk, t, out=kbuf, stream=ks)
-        torch.cuda.synchronize(dev)
-        if time.perf_counter() - tw >= args.clock_warm_s:
-            break
+    # time queued behind the other streams' kernels)
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
+    warm_clocks()
     for a, b in kev:
         a.record(ks)
         rd.render(fk, t, out=kbuf, stream=ks)
         b.record(ks)
     torch.cuda.synchronize(dev)
     kavg_ms = sum(a.elapsed_time(b) for a, b in kev) / len(kev)
-    del kbuf
     log(f"[bench] rank {rank}/{world} {args.config} {W}x{H} rows={rows} "
         f"precision={args.precision} warmup={args.warmup} steps={args.steps}")
     elapsed, kernel_ms, drv = timed_run(frame, args.steps, args.warmup)

@@ -426,9 +426,11 @@ int sdf_driver_frame(sdf_driver* driver, int64_t index, void** rgba);
  * all work queued for that frame. */
 int sdf_driver_read_frame(sdf_driver* driver, int64_t index, void* dst, int64_t bytes,
                           void* stream);
-/* Host-time accounting since creation: out[0] frames stepped, out[1]
- * seconds spent inside sdf_driver_step / sdf_driver_drain, out[2] the part
- * of out[1] spent waiting for the GPU or a peer (n >= 3). */
+/* Host-time accounting since creation (n >= 3 values): out[0] frames
+ * stepped, out[1] seconds spent inside sdf_driver_step / sdf_driver_drain,
+ * out[2] the part of out[1] spent waiting for the GPU or a peer; then the
+ * seconds spent enqueueing out[3] renders, out[4] length all-gathers (with
+ * their copies and events), out[5] RCCL send/recv groups, out[6] decodes. */
 int sdf_driver_stats(sdf_driver* driver, double* out, int32_t n);
 int sdf_driver_destroy(sdf_driver* driver);
 

@@ -144,6 +144,7 @@ struct sdf_driver {
   // host-time accounting (sdf_driver_stats): seconds inside step/drain, and
   // the part of it spent waiting for the GPU or a peer
   double t_calls = 0.0, t_wait = 0.0;
+  double t_render = 0.0, t_lengths = 0.0, t_group = 0.0, t_decode = 0.0;  // launches
   long long n_steps = 0;
 };
 
@@ -224,6 +225,7 @@ int ship(sdf_driver* d, long long j) {
   if (rc != SDF_OK) return fail(d, rc);
   const Rccl& R = *d->data_comm->api;
   ncclComm_t comm = d->data_comm->comm;
+  auto tg = Clock::now();
   rc = nccl_ok(R.GroupStart());
   if (rc == SDF_OK && d->sender)
     rc = nccl_ok(R.Send(d->local[b], (size_t)(d->data_off[d->rank] + sz[d->rank]), ncclUint8, 0,
@@ -234,13 +236,17 @@ int ship(sdf_driver* d, long long j) {
         rc = nccl_ok(R.Recv(static_cast<char*>(d->gathered[b]) + (size_t)r * d->pitch,
                             (size_t)(d->data_off[r] + sz[r]), ncclUint8, r, comm, d->ds));
   const int rc_end = nccl_ok(R.GroupEnd());
+  d->t_group += seconds_since(tg);
   if (rc == SDF_OK) rc = rc_end;
   if (rc != SDF_OK) return fail(d, rc);
   rc = hip_ok(hipEventRecord(d->ev_gather[b], d->ds));
   if (rc == SDF_OK) rc = hip_ok(hipStreamWaitEvent(d->rs[b], d->ev_gather[b], 0));
-  if (rc == SDF_OK && d->root)
+  if (rc == SDF_OK && d->root) {
+    tg = Clock::now();
     rc = hip_ok((hipError_t)sdf::launch_tiles_decode(d->decode, d->frames[b], d->gathered[b],
                                                      d->rs[b]));
+    d->t_decode += seconds_since(tg);
+  }
   return fail(d, rc);
 }
 
@@ -478,8 +484,10 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
   const int b = (int)(i % d->nbuf);
   hipStream_t s = d->rs[b];
   int rc = SDF_OK;
+  auto tr = Clock::now();
   if (d->sender) rc = sdf::launch_render_plan(d->plan_send[b], s);
   if (rc == SDF_OK && d->root && !d->sender) rc = sdf::launch_render_plan(d->plan_frame[b], s);
+  d->t_render += seconds_since(tr);
   if (rc != SDF_OK) return fail(d, rc);
   if (frame_index) *frame_index = i;
   d->next = i + 1;
@@ -494,6 +502,7 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
     if (rc != SDF_OK) return rc;
   }
   // the ranks' stream lengths of frame i, to every rank
+  tr = Clock::now();
   rc = hip_ok(hipStreamWaitEvent(d->ss, d->ev_render[b], 0));
   if (rc != SDF_OK) return fail(d, rc);
   int32_t* sz = d->sizes_dev + (size_t)b * d->world;
@@ -503,6 +512,7 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
     rc = hip_ok(hipMemcpyAsync(d->sizes_host + (size_t)b * d->world, sz,
                                sizeof(int32_t) * d->world, hipMemcpyDeviceToHost, d->ss));
   if (rc == SDF_OK) rc = hip_ok(hipEventRecord(d->ev_size[b], d->ss));
+  d->t_lengths += seconds_since(tr);
   if (rc != SDF_OK) return fail(d, rc);
   d->pending.push_back(i);
   return SDF_OK;
@@ -567,9 +577,9 @@ int sdf_driver_read_frame(sdf_driver* d, int64_t index, void* dst, int64_t bytes
 
 int sdf_driver_stats(sdf_driver* d, double* out, int32_t n) {
   if (!d || !out || n < 3) return SDF_E_INVALID_ARG;
-  out[0] = (double)d->n_steps;
-  out[1] = d->t_calls;
-  out[2] = d->t_wait;
+  const double v[7] = {(double)d->n_steps, d->t_calls, d->t_wait, d->t_render,
+                       d->t_lengths, d->t_group, d->t_decode};
+  for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
   return SDF_OK;
 }
 

@@ -135,11 +135,14 @@ class NativeFrameDriver:
     def stats(self) -> dict:
         """Host time of the driver's calls: frames, seconds in step/drain, and
         the seconds of that spent waiting on the GPU or a peer."""
-        out = (C.c_double * 3)()
-        abi.check(self.lib.sdf_driver_stats(self.handle, out, 3), "sdf_driver_stats")
+        out = (C.c_double * 7)()
+        abi.check(self.lib.sdf_driver_stats(self.handle, out, 7), "sdf_driver_stats")
         n = max(out[0], 1.0)
+        us = lambda x: round(x / n * 1e6, 2)  # noqa: E731
         return {"frames": int(out[0]), "call_s": out[1], "wait_s": out[2],
-                "host_us_per_frame": round((out[1] - out[2]) / n * 1e6, 2)}
+                "host_us_per_frame": us(out[1] - out[2]),
+                "enqueue_us_per_frame": {"render": us(out[3]), "lengths": us(out[4]),
+                                         "transfer_group": us(out[5]), "decode": us(out[6])}}
 
     def close(self) -> None:
         if self.handle:

@@ -177,7 +177,8 @@ def main():
         st = drv.stats()
         drv.close()
         return {"ms_per_frame": round(el / frames * 1e3, 4),
-                "host_us_per_frame": st["host_us_per_frame"]}
+                "host_us_per_frame": st["host_us_per_frame"],
+                "enqueue_us_per_frame": st["enqueue_us_per_frame"]}
 
     nat = {}
     for lag, nbuf in ((1, 3), (2, 4)):
