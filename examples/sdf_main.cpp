@@ -6,11 +6,87 @@
 // as a PPM instead of being presented in a window (:95-96).
 //
 //   sdf_main [width height frames out.ppm scene]     scene: ref | csg8 | bulb
+//
+// Multi-GPU: launched once per GPU by any launcher that sets RANK,
+// WORLD_SIZE and LOCAL_RANK (e.g. `torchrun --nproc-per-node 8 --no-python
+// sdf_main 3840 2160 200 out.ppm csg8`), or with SDF3D_DRIVER=1 on one GPU,
+// it runs the native frame driver (sdf_driver_*): every rank renders its row
+// blocks of every frame and rank 0 assembles them over RCCL.  The two RCCL
+// unique ids travel through files in SDF3D_ID_DIR (default /tmp) named by
+// SDF3D_RUN_ID (default: torchrun's TORCHELASTIC_RUN_ID); SDF3D_RCCL names
+// the librccl to load (default librccl.so.1); SDF3D_ROOT_AS_PEER=1 makes
+// rank 0 ship its rows to itself (the multi-rank sequence on one GPU).
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
 
 #include "../include/sdf3d.hpp"
+
+namespace {
+
+std::string env(const char* name, const char* dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? v : dflt;
+}
+
+int run_driver(sdf::Frame f, int frames, const std::string& out) {
+  const int rank = std::atoi(env("RANK", "0").c_str());
+  const int world = std::atoi(env("WORLD_SIZE", "1").c_str());
+  const int local = std::atoi(env("LOCAL_RANK", "0").c_str());
+  const bool peer_root = env("SDF3D_ROOT_AS_PEER", "0") == "1";
+  sdf::check_hip(hipSetDevice(local), "hipSetDevice");
+  const std::string rccl = env("SDF3D_RCCL", "librccl.so.1");
+  const std::string dir = env("SDF3D_ID_DIR", "/tmp");
+  const std::string run = env("SDF3D_RUN_ID", env("TORCHELASTIC_RUN_ID", "default").c_str());
+  std::unique_ptr<sdf::Comm> lengths, data;
+  if (world > 1 || peer_root) {
+    const std::string a = "sdf3d_" + run + "_lengths.id", b = "sdf3d_" + run + "_data.id";
+    lengths.reset(new sdf::Comm(sdf::exchange_id(dir, a, rank, rccl), world, rank, rccl));
+    data.reset(new sdf::Comm(sdf::exchange_id(dir, b, rank, rccl), world, rank, rccl));
+    if (rank == 0) {  // every rank has joined both communicators: the files are spent
+      std::remove((dir + "/" + a).c_str());
+      std::remove((dir + "/" + b).c_str());
+    }
+  }
+  // shares: SDF3D_SHARES="a:b", else what the cost model of bench.py picks
+  // for this world size (sdf3d_amd/multigpu.py choose_shares)
+  static const int kShares[9][2] = {{1, 1}, {1, 1}, {4, 3}, {1, 1}, {1, 1},
+                                    {3, 4}, {3, 4}, {1, 2}, {1, 2}};
+  int share_root = kShares[world < 9 ? world : 8][0], share_peer = kShares[world < 9 ? world : 8][1];
+  if (std::sscanf(env("SDF3D_SHARES", "").c_str(), "%d:%d", &share_root, &share_peer) != 2) {
+    share_root = kShares[world < 9 ? world : 8][0];
+    share_peer = kShares[world < 9 ? world : 8][1];
+  }
+  sdf_driver_config cfg = {rank, world, share_root, share_peer, world > 1 || peer_root ? 4 : 3,
+                           world > 1 || peer_root ? 2 : 1,
+                           peer_root ? SDF_DRIVER_ROOT_AS_PEER : 0, 60000};
+  f.params.output_format = SDF_FORMAT_RGBA32F;
+  sdf::FrameDriver drv(f, cfg, lengths.get(), data.get());
+  int64_t last = -1;
+  for (int i = 0; i < 5; ++i) last = drv.step();  // warm-up
+  drv.drain();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < frames; ++i) {
+    f.orbit(360.0f * i / frames, 0.0f);             // the arcball's V_mat (main.cpp:93-94)
+    drv.set_camera(f.camera);
+    last = drv.step();
+  }
+  drv.drain();
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (rank == 0) {
+    std::printf("rank 0 of %d: %d frames %dx%d in %.3f ms: %.1f fps, %.1f Mpixels/s "
+                "(driver host %.1f us/frame)\n",
+                world, frames, f.params.width, f.params.height, s * 1e3, frames / s,
+                double(f.params.width) * f.params.height * frames / s / 1e6,
+                drv.host_us_per_frame());
+    sdf::write_ppm(out, drv.download(last), f.params.width, f.params.height);
+    std::printf("wrote %s\n", out.c_str());
+  }
+  return 0;
+}
+
+}  // namespace
 
 int main(int argc, char** argv) {
   const int W = argc > 1 ? std::atoi(argv[1]) : 800;   // main.cpp:4 SX
@@ -43,6 +119,8 @@ int main(int argc, char** argv) {
       f.params.normal_mode = SDF_NORMAL_TETRA;
     }
     f.params.precision = SDF_PRECISION_FAST;
+    if (std::getenv("WORLD_SIZE") || env("SDF3D_DRIVER", "0") == "1")
+      return run_driver(f, frames, out);
 
     hipStream_t stream;
     sdf::check_hip(hipStreamCreate(&stream), "hipStreamCreate");

@@ -14,11 +14,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <cstdio>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sdf_abi.h"
@@ -173,6 +177,110 @@ class Renderer {
   int w_, h_;
   hipStream_t stream_;
   float* rgba_ = nullptr;
+};
+
+// ---- multi-device frames (sdf_comm_* / sdf_driver_*) ------------------------
+
+// One RCCL communicator over `world` processes (one per GPU), created from a
+// unique id rank 0 makes; the caller moves the id between processes.
+class Comm {
+ public:
+  using Id = std::vector<unsigned char>;
+  static Id unique_id(const std::string& rccl_path = "") {
+    Id id(SDF_COMM_ID_BYTES);
+    check(sdf_comm_unique_id(rccl_path.empty() ? nullptr : rccl_path.c_str(), id.data()),
+          "sdf_comm_unique_id");
+    return id;
+  }
+  Comm(const Id& id, int world, int rank, const std::string& rccl_path = "") {
+    check(sdf_comm_create(rccl_path.empty() ? nullptr : rccl_path.c_str(), id.data(), world, rank,
+                          &c_),
+          "sdf_comm_create");
+  }
+  ~Comm() { if (c_) (void)sdf_comm_destroy(c_); }
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+  sdf_comm* get() const { return c_; }
+
+ private:
+  sdf_comm* c_ = nullptr;
+};
+
+// Moves communicator ids through a directory every rank can see (a node's
+// local disk or /dev/shm): rank 0 writes `name` atomically (write, then
+// rename), the others wait for it.  Pure-C++ launches (no MPI, no Python)
+// use this; a Python host uses torch.distributed (sdf3d_amd/driver.py).
+inline Comm::Id exchange_id(const std::string& dir, const std::string& name, int rank,
+                            const std::string& rccl_path = "", double timeout_s = 120.0) {
+  const std::string path = dir + "/" + name;
+  if (rank == 0) {
+    Comm::Id id = Comm::unique_id(rccl_path);
+    const std::string tmp = path + ".tmp";
+    FILE* fp = std::fopen(tmp.c_str(), "wb");
+    if (!fp || std::fwrite(id.data(), 1, id.size(), fp) != id.size() || std::fclose(fp) != 0 ||
+        std::rename(tmp.c_str(), path.c_str()) != 0)
+      throw std::runtime_error("cannot write " + path);
+    return id;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    if (FILE* fp = std::fopen(path.c_str(), "rb")) {
+      Comm::Id id(SDF_COMM_ID_BYTES);
+      const size_t n = std::fread(id.data(), 1, id.size(), fp);
+      std::fclose(fp);
+      if (n == id.size()) return id;
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      throw std::runtime_error("timed out waiting for " + path);
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+}
+
+// The native frame loop across the node (include/sdf_abi.h sdf_driver_*):
+// every rank steps every frame; rank 0 holds the assembled frames.  The
+// reference's `while (!gl->closed()) { ... gl->plot(sh, proj_mode); }`
+// (main.cpp:87-98) becomes `while (...) { drv.set_camera(...); drv.step(); }`.
+class FrameDriver {
+ public:
+  FrameDriver(const Frame& f, const sdf_driver_config& cfg, Comm* lengths = nullptr,
+              Comm* data = nullptr)
+      : w_(f.params.width), h_(f.params.height), format_(f.params.output_format) {
+    check(sdf_driver_create(&f.scene, &f.camera, &f.light, &f.material, &f.params, &cfg,
+                            lengths ? lengths->get() : nullptr, data ? data->get() : nullptr, &d_),
+          "sdf_driver_create");
+  }
+  ~FrameDriver() { if (d_) (void)sdf_driver_destroy(d_); }
+  FrameDriver(const FrameDriver&) = delete;
+  FrameDriver& operator=(const FrameDriver&) = delete;
+
+  void set_camera(const sdf_camera& c) { check(sdf_driver_set_camera(d_, &c), "sdf_driver_set_camera"); }
+  int64_t step() {
+    int64_t i = -1;
+    check(sdf_driver_step(d_, &i), "sdf_driver_step");
+    return i;
+  }
+  void drain() { check(sdf_driver_drain(d_), "sdf_driver_drain"); }
+  // Rank 0: blocking copy of frame i (one of the last nbuf, shipped).
+  std::vector<float> download(int64_t i) const {
+    if (format_ != SDF_FORMAT_RGBA32F) throw Error(SDF_E_UNSUPPORTED, "download: not RGBA32F");
+    std::vector<float> out(size_t(w_) * h_ * 4);
+    void* src = nullptr;
+    check(sdf_driver_frame(d_, i, &src), "sdf_driver_frame");
+    check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    check_hip(hipMemcpy(out.data(), src, out.size() * sizeof(float), hipMemcpyDeviceToHost),
+              "hipMemcpy");
+    return out;
+  }
+  // Host seconds of the driver's own calls per frame, waits excluded.
+  double host_us_per_frame() const {
+    double v[3] = {0, 0, 0};
+    check(sdf_driver_stats(d_, v, 3), "sdf_driver_stats");
+    return v[0] > 0 ? (v[1] - v[2]) / v[0] * 1e6 : 0.0;
+  }
+
+ private:
+  int w_, h_, format_;
+  sdf_driver* d_ = nullptr;
 };
 
 // Binary PPM of an RGBA float framebuffer, clamped and quantised to 8 bits

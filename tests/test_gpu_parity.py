@@ -454,3 +454,31 @@ def test_culling_exact_on_random_scenes(renderer, seed):
     c, sc = gpu(renderer, g)
     assert_parity(report(a, sa, b, sb), what=f"seed {seed}")
     assert_parity(report(c, sc, b, sb), what=f"seed {seed} generic")
+
+
+@pytest.mark.parametrize("peer_root", [False, True])
+def test_cpp_frame_driver(renderer, tmp_path, peer_root):
+    """The C++ host program's native frame-driver mode (sdf::FrameDriver over
+    sdf_driver_*): whole frames at world 1, or with SDF3D_ROOT_AS_PEER=1 the
+    multi-rank sequence (TILES, RCCL length all-gather and send/recv to rank
+    0 = itself, decode) through a one-rank RCCL communicator whose ids travel
+    through files; the last frame equals the Python path's render."""
+    import os
+    import subprocess
+    exe = Path(__file__).resolve().parent.parent / "sdf3d_amd" / "bin" / "sdf_main"
+    out = tmp_path / "d.ppm"
+    env = dict(os.environ, SDF3D_DRIVER="1", SDF3D_ROOT_AS_PEER="1" if peer_root else "0",
+               SDF3D_ID_DIR=str(tmp_path), SDF3D_RUN_ID=f"t{os.getpid()}",
+               SDF3D_RCCL="/opt/rocm/lib/librccl.so.1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([str(exe), "160", "90", "2", str(out), "csg8"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "rank 0 of 1" in r.stdout
+    img = read_ppm(out)
+    f = scenes.config("C3", 160, 90, precision=abi.PRECISION_FAST)
+    scenes.set_view(f, scenes.orbit_view(180.0, 0.0))     # frame 1 of 2: yaw 180
+    rgba, _ = gpu(renderer, f, steps=False)
+    want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
+    assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
+    assert not list(tmp_path.glob("*.id")), "rank 0 removes the spent id files"
