@@ -25,71 +25,10 @@
 #include <stdint.h>
 
 #include "kernel_args.h"
+#include "wave_bits.h"
 
 namespace sdf {
 namespace {
-
-// Transpose of the 64 x 64 bit matrix whose row r is lane r's word (lo =
-// bits 0..31, hi = 32..63): on return lane c holds column c (bit r = bit c
-// of lane r's input).  Six butterfly stages exchange the off-diagonal j x j
-// blocks of every 2j x 2j block between lanes r and r ^ j:
-//   j = 32     one v_permlane32_swap (lanes 32..63 of lo <-> lanes 0..31 of hi);
-//   j <= 16    inside each 32-bit half: the partner's word (DPP quad_perm for
-//              j = 1, 2, ds_swizzle for 4, 8, 16) rotated by j toward this
-//              lane's blocks (v_alignbit, per-lane amount) and merged into
-//              them (v_bfi, per-lane mask).
-// A lane with bit j clear keeps its low blocks (mask m_j) and takes the
-// partner's low blocks shifted up by j; a lane with bit j set keeps its high
-// blocks and takes the partner's high blocks shifted down by j.
-struct TransposeLanes {
-  uint32_t keep[5], rot[5];   // stages j = 16, 8, 4, 2, 1
-  __device__ __forceinline__ explicit TransposeLanes(int lane) {
-    const uint32_t m[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int j = 16 >> i;
-      const bool upper = lane & j;
-      keep[i] = upper ? ~m[i] : m[i];
-      rot[i] = upper ? (uint32_t)j : (uint32_t)(32 - j);   // rotate right (rotl j = rotr 32 - j)
-    }
-  }
-};
-
-template <int J>
-__device__ __forceinline__ uint32_t xor_partner(uint32_t v) {
-  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
-  else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
-}
-
-// (a & mask) | (b & ~mask) in one v_bfi_b32 (the compiler splits it in two
-// when the mask's complement is live)
-__device__ __forceinline__ uint32_t bitfield_merge(uint32_t mask, uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
-  return r;
-}
-
-template <int I>
-__device__ __forceinline__ void transpose_stage(uint32_t& lo, uint32_t& hi, const TransposeLanes& T) {
-  constexpr int J = 16 >> I;
-  const uint32_t plo = xor_partner<J>(lo), phi = xor_partner<J>(hi);
-  const uint32_t qlo = __builtin_amdgcn_alignbit(plo, plo, T.rot[I]);
-  const uint32_t qhi = __builtin_amdgcn_alignbit(phi, phi, T.rot[I]);
-  lo = bitfield_merge(T.keep[I], lo, qlo);
-  hi = bitfield_merge(T.keep[I], hi, qhi);
-}
-
-__device__ __forceinline__ void transpose64(uint32_t& lo, uint32_t& hi, const TransposeLanes& T) {
-  const auto sw = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
-  lo = sw[0];
-  hi = sw[1];
-  transpose_stage<0>(lo, hi, T);
-  transpose_stage<1>(lo, hi, T);
-  transpose_stage<2>(lo, hi, T);
-  transpose_stage<3>(lo, hi, T);
-  transpose_stage<4>(lo, hi, T);
-}
 
 // Inclusive 2-D prefix sum (mod 2^32) over the 8 x 8 tile, lane = 8 row +
 // col.  Rows: DPP row_shr by 1, 2, 4 inside the 16-lane DPP rows, the
@@ -231,9 +170,11 @@ __global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
 // Offsets of the plane blocks in tile order: exclusive scan of 8 * (w0 + w1
 // + w2) over the heads.  tiles_scan: 256 threads x 8 consecutive tiles per
 // block of kScanTiles -> block-local offsets + the block's total.
-// tiles_move: one wave per tile adds its block's prefix (the sum of earlier
-// block totals, a wave reduction), writes the final offset, and copies its
-// planes from the slot into the stream; the last tile writes `used`.
+// tiles_move: one wave per 8 consecutive tiles (in one scan block) adds the
+// block's prefix (the sum of earlier block totals, a wave reduction), writes
+// the final offsets and copies the tiles' planes from their slots into the
+// stream, the 8 tiles' loads in flight together (one wave per tile took
+// 30.7 us on a whole 4K frame); the last tile writes `used`.
 __device__ __forceinline__ uint32_t plane_bytes(uint32_t widths) {
   return 8u * ((widths & 255u) + ((widths >> 8) & 255u) + ((widths >> 16) & 255u));
 }
@@ -271,28 +212,49 @@ __global__ __launch_bounds__(256) void tiles_scan(uint8_t* buf, int ntiles) {
     reinterpret_cast<uint32_t*>(buf + L.bsums)[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
+constexpr int kMoveTiles = 8;   // tiles per wave of tiles_move (divides kScanTiles)
+
 __global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles) {
   const TilesLayout L(ntiles);
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tile >= ntiles) return;
+  const int t0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kMoveTiles;
+  if (t0 >= ntiles) return;
   const int lane = threadIdx.x & 63;
-  const int blk = tile / kScanTiles;
+  const int nt = min(kMoveTiles, ntiles - t0);
+  const int blk = t0 / kScanTiles;   // all nt tiles lie in this scan block
   const uint32_t* bsums = reinterpret_cast<const uint32_t*>(buf + L.bsums);
   uint32_t pre = 0;
   for (int i = lane; i < blk; i += 64) pre += bsums[i];
 #pragma unroll
   for (int s = 32; s >= 1; s >>= 1) pre += (uint32_t)__shfl_xor((int)pre, s);
   uint32_t* table = reinterpret_cast<uint32_t*>(buf + L.table);
-  const uint32_t off = table[tile] + pre;
-  const uint32_t bytes = plane_bytes(reinterpret_cast<const uint4*>(buf + L.head)[tile].x);
-  const uint2* src = reinterpret_cast<const uint2*>(buf + L.slots + (size_t)tile * kTilePlaneBytes);
-  uint2* dst = reinterpret_cast<uint2*>(buf + L.data + off);
-  for (uint32_t i = lane; i < bytes / 8; i += 64) dst[i] = src[i];
-  if (lane == 0) {
-    table[tile] = off;
-    if (tile == ntiles - 1) {
-      reinterpret_cast<uint32_t*>(buf)[0] = off + bytes;
-      reinterpret_cast<uint32_t*>(buf)[1] = (uint32_t)ntiles;
+  // lane k < nt: tile t0 + k's block-local offset and plane bytes
+  const uint32_t loc = lane < nt ? table[t0 + lane] : 0u;
+  const uint32_t byt =
+      lane < nt ? plane_bytes(reinterpret_cast<const uint4*>(buf + L.head)[t0 + lane].x) : 0u;
+  const uint2* slots = reinterpret_cast<const uint2*>(buf + L.slots);
+  uint2* data = reinterpret_cast<uint2*>(buf + L.data);
+  constexpr int kQ = kTilePlaneBytes / 8;   // planes per slot
+  // every tile's first 64 planes in flight at once (lane i: plane i)
+  uint2 v[kMoveTiles];
+#pragma unroll
+  for (int k = 0; k < kMoveTiles; k++) {
+    const int nq = (int)((uint32_t)__builtin_amdgcn_readlane((int)byt, k) >> 3);
+    v[k] = lane < nq ? slots[(size_t)(t0 + k) * kQ + lane] : make_uint2(0u, 0u);
+  }
+#pragma unroll
+  for (int k = 0; k < kMoveTiles; k++) {
+    if (k >= nt) break;
+    const int nq = (int)((uint32_t)__builtin_amdgcn_readlane((int)byt, k) >> 3);
+    const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)loc, k) + pre;
+    if (lane < nq) data[off / 8 + lane] = v[k];
+    if (nq > 64 && lane + 64 < nq)   // planes 64..95 (residuals over 21 bits on average): rare
+      data[off / 8 + 64 + lane] = slots[(size_t)(t0 + k) * kQ + 64 + lane];
+    if (lane == 0) {
+      table[t0 + k] = off;
+      if (t0 + k == ntiles - 1) {
+        reinterpret_cast<uint32_t*>(buf)[0] = off + (uint32_t)nq * 8u;
+        reinterpret_cast<uint32_t*>(buf)[1] = (uint32_t)ntiles;
+      }
     }
   }
 }
@@ -304,7 +266,8 @@ int launch_tiles_compact(void* stream_buf, int ntiles, void* stream) {
   uint8_t* buf = reinterpret_cast<uint8_t*>(stream_buf);
   hipLaunchKernelGGL(tiles_scan, dim3((ntiles + kScanTiles - 1) / kScanTiles), dim3(256), 0,
                      (hipStream_t)stream, buf, ntiles);
-  hipLaunchKernelGGL(tiles_move, dim3((ntiles + 3) / 4), dim3(256), 0, (hipStream_t)stream, buf,
+  const int waves = (ntiles + kMoveTiles - 1) / kMoveTiles;
+  hipLaunchKernelGGL(tiles_move, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, buf,
                      ntiles);
   return (int)hipGetLastError();
 }
