@@ -56,7 +56,7 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 4
+#define SDF_ABI_VERSION 5   /* 5: escape-coded TILES streams */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -202,7 +202,7 @@ typedef struct {
  *            wire format for multi-device frames; sdf_deinterleave expands
  *            it to an RGBA32F frame with alpha = 1.
  *   TILES    RGB32F losslessly compressed for the multi-device gather (about
- *            4.4 instead of 12 bytes per pixel on the 4K CSG scene), decoded
+ *            3.2 instead of 12 bytes per pixel on the 4K CSG scene), decoded
  *            bit for bit by sdf_tiles_decode.  The rendered (packed) rows
  *            are cut into 8x8 tiles, tile t = ty * ceil(width / 8) + tx
  *            covering packed rows 8ty.. and columns 8tx..; pixel j = 8 *
@@ -212,21 +212,36 @@ typedef struct {
  *            residual u - left - up + upleft (neighbours outside the tile
  *            are 0; mod 2^32; its inverse is the tile's 2-D prefix sum),
  *            zigzag-coded to z, with z := 0 for pixel 0 (it travels raw) and
- *            for pixels outside the frame, stored as bit planes.
+ *            for pixels outside the frame.  Per channel c the tile stores
+ *            b[c] base bit planes (plane k holds bit k of z_j in bit j) and,
+ *            when its widest z has w > b[c] bits, an escape: a u64 mask of
+ *            the outlier pixels (z_j >= 2^b[c]), a width byte d = w - b[c]
+ *            and each outlier's bits b[c].. as a d-bit field.  The encoder
+ *            picks b[c] among w, w - 1, .., w - 12 by the smallest size
+ *            (64 b + 72 + d * outliers bits; ties: larger b).
  *            Stream layout (little-endian; sdf_tiles_bytes() sizes the
  *            buffer, stream plus the encoder's scratch):
- *              u32 used             bytes of bit-plane data
+ *              u32 used             bytes of tile data
  *              u32 ntiles
- *              u32 offset[ntiles]   tile t's planes at data + offset[t]
+ *              u32 offset[ntiles]   tile t's data at data + offset[t]
  *              head = stream + align16(8 + 4 * ntiles):
- *                u32x4 head[ntiles] {w0 | w1 << 8 | w2 << 16, first[3]}:
- *                                   w[c] the bit length of the tile's
- *                                   largest z, first[c] u of pixel 0
- *              data = head + 16 * ntiles: per tile w0 + w1 + w2 u64 planes,
- *                                   channel by channel, plane b holding
- *                                   bit b of z_j in bit j
- *            The meaningful prefix of a stream is data + used bytes; plane
- *            blocks appear in tile order.                                 */
+ *                u32x4 head[ntiles] {b0 | b1 << 6 | b2 << 12 | q << 18 |
+ *                                   e << 26, first[3]}: q the tile's data
+ *                                   in u64 words, e bit c set when channel
+ *                                   c is escaped (P = popcount(e)),
+ *                                   first[c] u of pixel 0
+ *              data = head + 16 * ntiles, per tile q u64 words:
+ *                                   b0 + b1 + b2 base planes, channel by
+ *                                   channel; the P masks of the escaped
+ *                                   channels; then one bitstream (LSB
+ *                                   first, zero-padded to whole words):
+ *                                   the P width bytes, then the fields
+ *                                   pixel by pixel, each pixel's fields of
+ *                                   the channels it is an outlier of in
+ *                                   channel order
+ *            The meaningful prefix of a stream is data + used bytes; tile
+ *            blocks appear in tile order (tests/tiles_ref.py states the
+ *            codec in NumPy).                                             */
 typedef enum {
   SDF_FORMAT_RGBA32F = 0,
   SDF_FORMAT_RGBA16F = 1,

@@ -108,6 +108,11 @@ struct TilesLayout {
   }
 };
 int launch_tiles_compact(void* stream_buf, int ntiles, void* stream);
+// A tile's head word 0 (sdf_abi.h SDF_FORMAT_TILES): base widths b0 | b1 << 6
+// | b2 << 12, the tile's data in qwords << 18, escaped channels << 26.
+__host__ __device__ inline uint32_t tile_qwords(uint32_t head) { return (head >> 18) & 255u; }
+constexpr int kEscapeWindow = 12;   // base widths tried below the widest residual
+constexpr int kEscapeDwords = 72;   // bitstream bound: 3 width bytes + 3 x 12 x 63 bits
 // run-time specialised kernel for a scene signature (jit.cpp); -1 = none
 int launch_render_jit(const KernelArgs& a, const int* sig, int n, bool exact, void* stream);
 int jit_compiled_count();

@@ -58,7 +58,9 @@ __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
   return (u & 0x80000000u) ? (u ^ 0x7fffffffu) : u;
 }
 
-constexpr int kDecodeTiles = 4;   // tiles per wave of the decoder (4, 8: same speed; 16: slower)
+// tiles per wave of the decoder: 4 (0.051 ms for the root's 7/8 of a 4K
+// frame) beats 2 (0.055); forcing 8 waves / SIMD spills and gains nothing
+constexpr int kDecodeTiles = 4;
 
 // One wave = TPW consecutive tiles of one part, lane j = pixel (j / 8, j % 8)
 // of each.  The memory traffic is issued up front in two dependent rounds:
@@ -68,9 +70,8 @@ constexpr int kDecodeTiles = 4;   // tiles per wave of the decoder (4, 8: same s
 // concatenation), cut out the three channels, un-zigzag, 2-D prefix sum,
 // RGBA32F store into the tile's frame rows.
 template <int TPW>
-__global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
-                                                    const uint8_t* __restrict__ parts,
-                                                    int waves_per_part, float4* __restrict__ frame) {
+__device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t* __restrict__ parts,
+                                            int waves_per_part, float4* __restrict__ frame) {
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int part = gw / waves_per_part;
@@ -91,15 +92,12 @@ __global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
                               : make_uint4(0u, 0u, 0u, 0u);
   if (present == 0) return;   // no stream: rows rendered in place
   const uint2* data = reinterpret_cast<const uint2*>(base + Lt.data);
-  auto nplanes_of = [](uint32_t w) {
-    return (int)((w & 255) + ((w >> 8) & 255) + ((w >> 16) & 255));
-  };
-  uint2 pa[TPW];
+  uint2 pa[TPW];   // lane i: qword i of each tile's data (up to 64)
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
-    const int np = k < nt ? nplanes_of(__builtin_amdgcn_readlane((int)hdv.x, k)) : 0;
+    const int nq = k < nt ? (int)tile_qwords(__builtin_amdgcn_readlane((int)hdv.x, k)) : 0;
     const uint32_t off = __builtin_amdgcn_readlane((int)offv, k);
-    pa[k] = lane < np ? data[off / 8 + lane] : make_uint2(0u, 0u);
+    pa[k] = lane < nq ? data[off / 8 + lane] : make_uint2(0u, 0u);
   }
   const TransposeLanes TL(lane);
   const ScanLanes SL(lane);
@@ -123,13 +121,16 @@ __global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
         ++blk;
       }
     }
-    const uint32_t widths = __builtin_amdgcn_readlane((int)hdv.x, k);
-    const int np = nplanes_of(widths);
-    uint32_t a0 = pa[k].x, a1 = pa[k].y, b0 = 0u, b1 = 0u;   // concatenation bits 0..63, 64..95
+    const uint32_t head = __builtin_amdgcn_readlane((int)hdv.x, k);
+    const int bw[3] = {(int)(head & 63), (int)((head >> 6) & 63), (int)((head >> 12) & 63)};
+    const int nq = (int)tile_qwords(head);
+    const uint32_t escaped = (head >> 26) & 7;
+    const int B = bw[0] + bw[1] + bw[2];
+    const uint2* tdata = data + __builtin_amdgcn_readlane((int)offv, k) / 8;
+    uint32_t a0 = pa[k].x, a1 = pa[k].y, b0 = 0u, b1 = 0u;   // base bits 0..63, 64..95
     transpose64(a0, a1, TL);
-    if (np > 64) {   // planes 64..95: rare (residuals wider than 21 bits on average)
-      const uint2 pb = lane + 64 < np ? data[__builtin_amdgcn_readlane((int)offv, k) / 8 + 64 + lane]
-                                      : make_uint2(0u, 0u);
+    if (B > 64) {   // base planes 64..95: rare (residuals wider than 21 bits on average)
+      const uint2 pb = lane + 64 < B ? tdata[64 + lane] : make_uint2(0u, 0u);
       b0 = pb.x;
       b1 = pb.y;
       transpose64(b0, b1, TL);
@@ -137,17 +138,70 @@ __global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
     const uint32_t first[3] = {(uint32_t)__builtin_amdgcn_readlane((int)hdv.y, k),
                                (uint32_t)__builtin_amdgcn_readlane((int)hdv.z, k),
                                (uint32_t)__builtin_amdgcn_readlane((int)hdv.w, k)};
+    // the escapes: masks at qwords B.., then the field-width bytes and the
+    // pixel-major fields, a bitstream from qword B + P (P escaped channels):
+    // this pixel's fields (all its escaped channels) are one window of <= 36
+    // bits at bit 8 P + sum_c d_c * (outliers of c below this pixel)
+    const int P = __builtin_popcount(escaped);
+    uint64_t m[3] = {0ull, 0ull, 0ull}, fields = 0ull;
+    int dlt[3] = {0, 0, 0};
+    if (escaped) {
+      const int bs = 2 * (B + P);                       // bitstream's first dword
+      const uint32_t deltas = bs < 128 ? (uint32_t)__builtin_amdgcn_readlane(
+                                             (int)((bs & 1) ? pa[k].y : pa[k].x), bs >> 1)
+                                       : reinterpret_cast<const uint32_t*>(tdata)[bs];
+      uint32_t o = 8u * (uint32_t)P;
+      int nb = 0, j = 0;
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) {
+        if (!((escaped >> ch) & 1)) continue;
+        const int mq = B + j;
+        if (mq < 64) {
+          m[ch] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pa[k].x, mq) |
+                  (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pa[k].y, mq) << 32;
+        } else {
+          const uint2 mm = tdata[mq];
+          m[ch] = (uint64_t)mm.x | (uint64_t)mm.y << 32;
+        }
+        dlt[ch] = (int)((deltas >> (8 * j++)) & 255);
+        o += (uint32_t)dlt[ch] * __builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(m[ch] >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m[ch], 0u));
+        if ((m[ch] >> lane) & 1) nb += dlt[ch];
+      }
+      // dwords dw .. dw + 2 of the tile's data: qwords dw / 2 and dw / 2 + 1
+      // from the lanes holding them
+      const uint32_t dw = (uint32_t)bs + (o >> 5);
+      const int a = (int)((dw >> 1) << 2);
+      const uint32_t s0 = __builtin_amdgcn_ds_bpermute(a, (int)pa[k].x);
+      const uint32_t s1 = __builtin_amdgcn_ds_bpermute(a, (int)pa[k].y);
+      const uint32_t t0 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].x);
+      const uint32_t t1 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].y);
+      uint32_t d0 = (dw & 1) ? s1 : s0, d1 = (dw & 1) ? t0 : s1, d2 = (dw & 1) ? t1 : t0;
+      if (nb && dw + 2 >= 128) {   // beyond the loaded qwords: rare
+        const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
+        d0 = t32[dw];
+        d1 = t32[dw + 1];
+        d2 = t32[dw + 2];
+      }
+      fields = (uint64_t)__builtin_amdgcn_alignbit(d1, d0, o & 31) |
+               (uint64_t)__builtin_amdgcn_alignbit(d2, d1, o & 31) << 32;
+    }
     float v[3];
     int kp = 0;
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
-      const int w = (widths >> (8 * ch)) & 255;
-      // 32 bits of the concatenation from bit kp (kp, w wave-uniform)
+      const int w = bw[ch];
+      // w bits of the base concatenation from bit kp (kp, w wave-uniform)
       const uint32_t x = kp < 32   ? __builtin_amdgcn_alignbit(a1, a0, kp)
                          : kp < 64 ? __builtin_amdgcn_alignbit(b0, a1, kp - 32)
                                    : __builtin_amdgcn_alignbit(b1, b0, kp - 64);
-      const uint32_t z = w ? x & (0xFFFFFFFFu >> (32 - w)) : 0u;
+      uint32_t z = w ? x & (0xFFFFFFFFu >> (32 - w)) : 0u;
       kp += w;
+      if ((m[ch] >> lane) & 1) {   // this pixel's next field: bits w.. of z
+        z |= ((uint32_t)fields & (0xFFFFFFFFu >> (32 - dlt[ch]))) << w;
+        fields >>= dlt[ch];
+      }
       uint32_t r = (z >> 1) ^ (0u - (z & 1u));            // un-zigzag
       if (lane == 0) r = first[ch];                       // pixel 0 travels raw
       v[ch] = __uint_as_float(unordered_bits(scan_tile(r, SL)));
@@ -164,7 +218,14 @@ __global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
       const int y = (first_blk + b * period) * brows + w;
       frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
     }
+    (void)nq;
   }
+}
+
+__global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
+                                                    const uint8_t* __restrict__ parts,
+                                                    int waves_per_part, float4* __restrict__ frame) {
+  decode_body<kDecodeTiles>(D, parts, waves_per_part, frame);
 }
 
 // Offsets of the plane blocks in tile order: exclusive scan of 8 * (w0 + w1
@@ -175,9 +236,7 @@ __global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
 // the final offsets and copies the tiles' planes from their slots into the
 // stream, the 8 tiles' loads in flight together (one wave per tile took
 // 30.7 us on a whole 4K frame); the last tile writes `used`.
-__device__ __forceinline__ uint32_t plane_bytes(uint32_t widths) {
-  return 8u * ((widths & 255u) + ((widths >> 8) & 255u) + ((widths >> 16) & 255u));
-}
+__device__ __forceinline__ uint32_t plane_bytes(uint32_t head) { return 8u * tile_qwords(head); }
 
 __global__ __launch_bounds__(256) void tiles_scan(uint8_t* buf, int ntiles) {
   const TilesLayout L(ntiles);
@@ -280,7 +339,7 @@ int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, vo
   const int waves_per_part = (tiles_per_part + kDecodeTiles - 1) / kDecodeTiles;
   const long long waves = (long long)waves_per_part * d.nparts;
   if (waves == 0) return 0;
-  hipLaunchKernelGGL((decode_tiles<kDecodeTiles>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(decode_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, d, reinterpret_cast<const uint8_t*>(parts),
                      waves_per_part, reinterpret_cast<float4*>(frame));
   return (int)hipGetLastError();

@@ -79,25 +79,27 @@ def owned_rows_py(height: int, rank: int, world: int, block_rows: int = 8,
 # Per-frame costs of the 4K CSG frame (C4) on one MI355X, in ms of one whole
 # frame (tools/root_probe.py, profiles/r01_root_probe_C4.json): the rows
 # rendered straight into the frame; the rows rendered as a TILES stream
-# (render + encoding); the TILES decode; the floor of a small share's render
-# (its launch ends with its slowest tiles even on alternating streams: 1/15
-# and 1/22 of the frame both take ~0.027 ms); and the wire: the whole
-# frame's TILES stream (~4.4 B/pixel, 36.5 MB) over one xGMI link at ~77 GB/s
-# per direction (half the 153 GB/s link figure of MI355X_MICROARCH.md) --
-# every peer ships its share to rank 0 over its own link, concurrently.
-FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.44, "decode": 0.040, "floor": 0.026,
-                  "wire": 0.474}
+# (render + encoding); the TILES decode; the floor of a lone small render
+# (its launch ends with its slowest tiles: 1/15 and 1/22 of the frame both
+# take ~0.027 ms alone, but beside the decode, as rank 0 runs them, the
+# tail overlaps and the two simply add); and the wire: the whole frame's
+# TILES stream (3.21 B/pixel, 26.6 MB) over one xGMI link at ~65 GB/s per
+# direction (85% of half the 153 GB/s bidirectional link figure) -- every
+# peer ships its share to rank 0 over its own link, concurrently.
+FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.455, "decode": 0.0505, "floor": 0.026,
+                  "wire": 0.41}
 
 
 def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int]:
     """Shares (a, b) for the TILES frame driver: rank 0 renders its rows in
     place and decodes everyone else's, so it gets fewer rows.  Minimises the
-    larger of rank 0's per-frame work, max(a/P render, floor) + (1 - a/P)
-    decode, and a peer's, max(b/P render_tiles, floor, b/P wire) (P = a + b
+    larger of rank 0's per-frame work, max(a/P render + (1 - a/P) decode,
+    floor), and a peer's, max(b/P render_tiles, floor, b/P wire) (P = a + b
     (world - 1): a peer's frames are pipelined, so its period is the slower of
     its render and its link); ties go to the shorter period.  Measured at
-    N = 8 (rank 0 / busiest peer GPU work, ms per frame): 1:1 0.078 / 0.056,
-    1:2 0.060 / 0.059, 1:3 0.054 / 0.062."""
+    N = 8 (rank 0 / busiest peer GPU work, ms per frame, escape-coded TILES):
+    1:1 0.087 / 0.055, 1:2 0.068 / 0.059, 1:3 0.062 / 0.062, 1:4 0.059 /
+    0.062, 2:7 0.060 / 0.064 (profiles/r01_root_probe_C4.json)."""
     c = costs or FRAME_COSTS_MS
     if world <= 1:
         return (1, 1)
@@ -109,7 +111,7 @@ def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int
                     continue
                 P = a + b * (world - 1)
                 floor = c.get("floor", 0.0)
-                root = max(a / P * c["render"], floor) + (1 - a / P) * c["decode"]
+                root = max(a / P * c["render"] + (1 - a / P) * c["decode"], floor)
                 peer = max(b / P * c["render_tiles"], floor, b / P * c.get("wire", 0.0))
                 t = max(root, peer)
                 if best is None or t < best[0] * (1 - 1e-6):

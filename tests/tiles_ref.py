@@ -57,6 +57,42 @@ def _bit_length(m: np.ndarray) -> np.ndarray:
     return w
 
 
+# Per channel the tile keeps `b` base bit planes of every residual and, when
+# some residuals are wider (the tile's widest has `w` bits), an escape for
+# them: the 64-bit mask M of those pixels, a width byte w - b, and their
+# bits b..w-1 as (w - b)-bit fields.  b is the cheapest of w, w-1, ...,
+# w - ESCAPE_WINDOW (>= 0) in bits: 64 b, plus 64 + 8 + (w - b) n with n
+# outliers; ties keep the larger b.  The fields are ordered pixel-major:
+# pixel by pixel, each pixel's fields of the escaped channels it is an
+# outlier of, in channel order -- so pixel j's fields start at bit
+# 8 P + sum_c (w_c - b_c) * |{outliers of c below j}|.
+ESCAPE_WINDOW = 12
+
+
+def _choose_base(bl: np.ndarray) -> np.ndarray:
+    """[n, 64] bit lengths -> [n] base widths b."""
+    w = bl.max(axis=1)
+    best_b, best = w.copy(), 64 * w
+    for d in range(1, ESCAPE_WINDOW + 1):
+        b = w - d
+        n = (bl > np.maximum(b, 0)[:, None]).sum(axis=1)
+        cost = 64 * np.maximum(b, 0) + 72 + d * n
+        take = (b >= 0) & (cost < best)
+        best = np.where(take, cost, best)
+        best_b = np.where(take, b, best_b)
+    return best_b
+
+
+def _pack_fields(fields) -> bytes:
+    """[(value, nbits)] -> little-endian bitstream padded to whole qwords."""
+    acc, nbits = 0, 0
+    for v, k in fields:
+        acc |= (int(v) & ((1 << k) - 1)) << nbits
+        nbits += k
+    nq = (nbits + 63) // 64
+    return acc.to_bytes(8 * nq, "little")
+
+
 def encode(rgb: np.ndarray) -> np.ndarray:
     """[rows, width, >=3] float32 -> uint8 stream."""
     rows, width = rgb.shape[:2]
@@ -64,8 +100,7 @@ def encode(rgb: np.ndarray) -> np.ndarray:
     n = ty * tx
     inside = _tiles(np.ones((rows, width), dtype=np.uint8), rows, width).reshape(n, 64) == 1
     heads = np.zeros((n, 4), dtype=np.uint32)
-    planes_c, widths = [], []
-    bitpos = np.arange(64, dtype=np.uint64)
+    zs, bls, bases = [], [], []
     for c in range(3):
         u = ordered(np.ascontiguousarray(rgb[..., c], dtype=np.float32).view(np.uint32))
         t = _tiles(u, rows, width).astype(np.uint64)
@@ -78,21 +113,40 @@ def encode(rgb: np.ndarray) -> np.ndarray:
         heads[:, 1 + c] = t.reshape(n, 64)[:, 0].astype(np.uint32)
         z[:, 0] = 0
         z[~inside] = 0
-        w = _bit_length(z.max(axis=1))
-        planes = np.zeros((n, 32), dtype=np.uint64)
-        for b in range(32):
-            bits = (z >> np.uint64(b)) & np.uint64(1)
-            planes[:, b] = (bits << bitpos).sum(axis=1, dtype=np.uint64)
-        planes_c.append(planes)
-        widths.append(w)
-    heads[:, 0] = (widths[0] | widths[1] << 8 | widths[2] << 16).astype(np.uint32)
+        bl = _bit_length(z)
+        zs.append(z)
+        bls.append(bl)
+        bases.append(_choose_base(bl))
+    bitpos = np.arange(64, dtype=np.uint64)
     table = np.zeros(n, dtype=np.uint32)
     blocks, off = [], 0
     for i in range(n):
-        blk = np.concatenate([planes_c[c][i, :widths[c][i]] for c in range(3)])
+        base_planes, masks, deltas, fields = [], [], [], []
+        present = 0
+        outl = []
+        for c in range(3):
+            z, b = zs[c][i], int(bases[c][i])
+            w = int(bls[c][i].max())
+            for p in range(b):
+                base_planes.append(int((((z >> np.uint64(p)) & np.uint64(1)) << bitpos).sum(dtype=np.uint64)))
+            if b < w:
+                present |= 1 << c
+                o = bls[c][i] > b
+                outl.append((c, b, w - b, o))
+                masks.append(int(sum(1 << int(j) for j in np.nonzero(o)[0])))
+                deltas.append((w - b, 8))
+        for j in range(64):
+            for c, b, d, o in outl:
+                if o[j]:
+                    fields.append((int(zs[c][i][j]) >> b, d))
+        data = (np.array(base_planes + masks, dtype=np.uint64).tobytes()
+                + _pack_fields(deltas + fields))
+        nq = len(data) // 8
+        heads[i, 0] = (int(bases[0][i]) | int(bases[1][i]) << 6 | int(bases[2][i]) << 12
+                       | nq << 18 | present << 26)
         table[i] = off
-        blocks.append(blk.tobytes())
-        off += 8 * blk.size
+        blocks.append(data)
+        off += len(data)
     out = np.zeros(data_offset(n) + off, dtype=np.uint8)
     out[:8] = np.frombuffer(np.array([off, n], dtype=np.uint32).tobytes(), dtype=np.uint8)
     out[8:8 + 4 * n] = np.frombuffer(table.tobytes(), dtype=np.uint8)
@@ -115,24 +169,43 @@ def decode(stream: np.ndarray, width: int, rows: int) -> np.ndarray:
     out = np.ones((ty * 8, tx * 8, 4), dtype=np.float32)
     bitpos = np.arange(64, dtype=np.uint64)
     for i in range(n):
-        ws = [int(heads[i, 0]) & 255, int(heads[i, 0]) >> 8 & 255, int(heads[i, 0]) >> 16 & 255]
+        h = int(heads[i, 0])
+        bs = [h & 63, h >> 6 & 63, h >> 12 & 63]
+        nq, present = h >> 18 & 255, h >> 26 & 7
+        if int(table[i]) + 8 * nq > used:
+            raise ValueError("tile data beyond the used bytes")
         k = base + int(table[i])
-        if int(table[i]) + 8 * sum(ws) > used:
-            raise ValueError("planes beyond the used bytes")
+        q = np.frombuffer(s[k:k + 8 * nq].tobytes(), dtype=np.uint64)
+        pc = [c for c in range(3) if present >> c & 1]
+        B, P = sum(bs), len(pc)
+        bits = int.from_bytes(q[B + P:].tobytes(), "little")
+        deltas = {c: bits >> (8 * j) & 255 for j, c in enumerate(pc)}
+        masks = {c: int(q[B + j]) for j, c in enumerate(pc)}
+        zs = []
+        kp = 0
+        for c in range(3):
+            z = np.zeros(64, dtype=np.uint64)
+            for p in range(bs[c]):
+                z |= ((q[kp + p] >> bitpos) & np.uint64(1)) << np.uint64(p)
+            kp += bs[c]
+            zs.append(z)
+        pos = 8 * P
+        for j in range(64):
+            for c in pc:
+                if masks[c] >> j & 1:
+                    d = deltas[c]
+                    zs[c][j] |= np.uint64((bits >> pos & ((1 << d) - 1)) << bs[c])
+                    pos += d
         yi, xi = divmod(i, tx)
         for c in range(3):
-            planes = np.frombuffer(s[k:k + 8 * ws[c]].tobytes(), dtype=np.uint64)
-            k += 8 * ws[c]
-            z = np.zeros(64, dtype=np.uint64)
-            for b, p in enumerate(planes):
-                z |= ((p >> bitpos) & np.uint64(1)) << np.uint64(b)
+            z = zs[c]
             zi = z.astype(np.int64)
             r = np.where(zi & 1, -(zi >> 1) - 1, zi >> 1)             # unzigzag
             r = (r & 0xFFFFFFFF).astype(np.uint64)
             r[0] = int(heads[i, 1 + c])
             u = r.reshape(8, 8).cumsum(axis=0).cumsum(axis=1) & np.uint64(0xFFFFFFFF)
-            bits = ordered(u.astype(np.uint32))
-            out[yi * 8:yi * 8 + 8, xi * 8:xi * 8 + 8, c] = bits.view(np.float32)
+            fb = ordered(u.astype(np.uint32))
+            out[yi * 8:yi * 8 + 8, xi * 8:xi * 8 + 8, c] = fb.view(np.float32)
     return out[:rows, :width]
 
 

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C4")
     ap.add_argument("--n", type=int, default=50)
+    ap.add_argument("--whole-only", action="store_true")
     args = ap.parse_args()
     import torch
     from sdf3d_amd import Renderer, abi, renderer as R, scenes
@@ -47,9 +48,14 @@ def main():
     for name, t in [("whole", None), ("half_of_2", R.tiling(1, 2, 8)),
                     ("share_3_of_7_N2", R.tiling(1, 2, 8, shares=(4, 3))),
                     ("quarter_of_4", R.tiling(1, 4, 8)),
-                    ("share_2_of_15_N8", R.tiling(1, 8, 8, shares=(1, 2)))]:
+                    ("share_2_of_15_N8", R.tiling(1, 8, 8, shares=(1, 2)))][:1 if args.whole_only else 5]:
         p, q = timed(plain, t, args.n), timed(tiles, t, args.n)
         out[name] = {"rgba32f_ms": p, "tiles_ms": q, "overhead": round(q / p - 1, 4)}
+        if t is None:
+            st, _ = rd.render(tiles)
+            torch.cuda.synchronize()
+            W, H = plain.params.width, plain.params.height
+            out[name]["stream_bytes_per_px"] = round(R.tiles_stream_bytes(st) / (W * H), 4)
     print(json.dumps(out, indent=1))
 
 
