@@ -4,11 +4,14 @@
 One step = one frame of BASELINE.json's workload (default C4: the 8-primitive
 smooth-min CSG scene with soft shadows, 5-tap AO and tetrahedral normals at
 3840x2160, 128 max steps), rendered by the HIP kernel through the C-ABI
-(sdf_render).  With N ranks (one process per GPU, torchrun) each rank renders
-its interleaved 8-row blocks of the frame and the blocks are gathered to rank 0
-over RCCL and scattered into the frame (sdf_deinterleave); the gather of
-frame i overlaps the render of frame i+1 (double-buffered).  Total work per
-step is one frame whatever N is ("scaling": "strong").
+(sdf_render), looped by the native frame driver (sdf_driver_*, C++).  With N
+ranks (one process per GPU, torchrun) each rank renders its interleaved 8-row
+blocks of the frame (rank 0 fewer: multigpu.choose_shares); the peers ship
+them as lossless TILES streams to rank 0 over RCCL, and rank 0 decodes them
+straight into the frame (sdf_tiles_decode_tilings).  Frames are pipelined
+over 4 buffer sets on alternating streams: frame i ships while frames i+1,
+i+2 render.  Total work per step is one frame whatever N is ("scaling":
+"strong").
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
                     [--precision fast|exact] [--no-cpu-baseline]
