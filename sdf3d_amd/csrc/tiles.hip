@@ -19,7 +19,7 @@
 //               columns) invert the gradient predictor in uint32 arithmetic.
 //
 // All three move a few bytes per pixel; the decode writes 16 per pixel
-// (RGBA32F) and runs ~130 VALU instructions per 8 x 8 tile.
+// (RGBA32F); the decode is VALU-issue bound (TILES).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -73,7 +73,10 @@ template <int TPW>
 __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t* __restrict__ parts,
                                             int waves_per_part, float4* __restrict__ frame) {
   const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // the wave index as a scalar: from threadIdx.x the compiler cannot tell it
+  // is wave-uniform and would run all tile / part arithmetic (divisions
+  // included) on the VALU
+  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int part = gw / waves_per_part;
   if (part >= D.nparts) return;
   const int tbase = (gw - part * waves_per_part) * TPW;
@@ -275,7 +278,7 @@ constexpr int kMoveTiles = 8;   // tiles per wave of tiles_move (divides kScanTi
 
 __global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles) {
   const TilesLayout L(ntiles);
-  const int t0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kMoveTiles;
+  const int t0 = (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * kMoveTiles;
   if (t0 >= ntiles) return;
   const int lane = threadIdx.x & 63;
   const int nt = min(kMoveTiles, ntiles - t0);

@@ -7,14 +7,14 @@ SURVEY.md 8(e), where contiguous bands are 1.75x), packed densely.  Rank 0
 gathers the N parts and assembles the frame.  With the TILES wire the
 shares can be unequal (shares = (a, b): rank 0 owns a blocks and every other
 rank b per period of a + b (N - 1), choose_shares): rank 0 also decodes the
-other ranks' streams, so at N = 8 it gets 1 block in 15.  The reference has no
+other ranks' streams, so at N = 8 it gets 1 block in 22.  The reference has no
 multi-device path at all (one GL context, /root/reference/Code/src/main.cpp:48,53).
 
 Wire formats (what crosses xGMI):
   "raw"    the packed rows themselves (RGBA, or RGB32F with alpha restored),
            scattered into the frame by sdf_deinterleave.
   "tiles"  the TILES stream (include/sdf_abi.h): lossless compressed RGB32F,
-           ~4.4 instead of 12 bytes per pixel on the 4K CSG frame, written by
+           ~3.2 instead of 12 bytes per pixel on the 4K CSG frame, written by
            the render kernel and decoded straight into the frame rows by
            sdf_tiles_decode.  Streams vary in length, so the ranks agree on
            each frame's byte count (an all-reduce MAX of one integer) before
@@ -79,14 +79,15 @@ def owned_rows_py(height: int, rank: int, world: int, block_rows: int = 8,
 # Per-frame costs of the 4K CSG frame (C4) on one MI355X, in ms of one whole
 # frame (tools/root_probe.py, profiles/r01_root_probe_C4.json): the rows
 # rendered straight into the frame; the rows rendered as a TILES stream
-# (render + encoding); the TILES decode; the floor of a lone small render
+# (render + encoding); the TILES decode (0.047 alone, 0.043 beside rank 0's
+# own render: rank 0's per-frame time minus its render share); the floor of a lone small render
 # (its launch ends with its slowest tiles: 1/15 and 1/22 of the frame both
 # take ~0.027 ms alone, but beside the decode, as rank 0 runs them, the
 # tail overlaps and the two simply add); and the wire: the whole frame's
 # TILES stream (3.21 B/pixel, 26.6 MB) over one xGMI link at ~65 GB/s per
 # direction (85% of half the 153 GB/s bidirectional link figure) -- every
 # peer ships its share to rank 0 over its own link, concurrently.
-FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.455, "decode": 0.0505, "floor": 0.026,
+FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.444, "decode": 0.043, "floor": 0.026,
                   "wire": 0.41}
 
 
@@ -98,8 +99,8 @@ def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int
     (world - 1): a peer's frames are pipelined, so its period is the slower of
     its render and its link); ties go to the shorter period.  Measured at
     N = 8 (rank 0 / busiest peer GPU work, ms per frame, escape-coded TILES):
-    1:1 0.087 / 0.055, 1:2 0.068 / 0.059, 1:3 0.062 / 0.062, 1:4 0.059 /
-    0.062, 2:7 0.060 / 0.064 (profiles/r01_root_probe_C4.json)."""
+    1:2 0.064 / 0.057, 1:3 0.058 / 0.060, 1:4 0.055 / 0.061, 2:7 0.055 /
+    0.062 (profiles/r01_root_probe_C4.json)."""
     c = costs or FRAME_COSTS_MS
     if world <= 1:
         return (1, 1)
