@@ -335,9 +335,10 @@ def test_cpp_host_program(renderer, tmp_path, scene_name, cfg):
 
 
 @pytest.mark.parametrize("nproc,wire,shares", [(2, "auto", None), (3, "auto", None),
-                                               (2, "rgb32f", None), (3, "tiles", "1:2")])
+                                               (2, "rgb32f", None), (3, "tiles", "1:2"),
+                                               (8, "auto", None)])
 def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire, shares):
-    """bench.py with 2-3 ranks sharing this GPU (gloo backend; RCCL needs one
+    """bench.py with 2, 3 or 8 ranks sharing this GPU (gloo backend; RCCL needs one
     GPU per rank): the FrameDriver's GPU path -- alternating render streams,
     the TILES wire (auto: kernel-written compressed streams, per-frame size
     agreement, sdf_tiles_decode_tilings on the frame's render stream of rank
@@ -366,6 +367,8 @@ def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire, shares):
     assert d["no_gather"]["value"] > 0
     if shares:
         assert d["config"]["tiling"].startswith("8-row blocks, rank 0 1 / others 2")
+    if nproc == 8:  # the round-end N=8 run's default shares (multigpu.choose_shares)
+        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 1 / others 3")
 
 
 def turbo_ref(steps, which, max_steps):
