@@ -56,7 +56,7 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 5   /* 5: escape-coded TILES streams */
+#define SDF_ABI_VERSION 6   /* 6: sdf_tiling.run_step (interleaved runs) */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -264,21 +264,26 @@ typedef enum {
 
 /* Which rows of the frame a call renders.  Rows are grouped into blocks of
  * `block_rows` rows; block b (rows [b*block_rows, (b+1)*block_rows)) is
- * rendered iff b >= first_block and (b - first_block) % block_stride <
- * run, with run = max(block_run, 1) consecutive blocks per period of
- * `block_stride` blocks.  Rendered rows are written densely ("packed") in
- * increasing y order, so {block_rows = 8, first_block = r, block_stride = N}
- * is device r's share of an N-device interleaved tiling and {8, 0, 1} is the
- * whole frame; runs give devices unequal shares (the multi-device frame
+ * rendered iff b >= first_block and, with o = (b - first_block) %
+ * block_stride, o % step == 0 and o / step < run: run = max(block_run, 1)
+ * blocks per period of `block_stride` blocks, step = max(run_step, 1) blocks
+ * apart (step 1: consecutive).  Rendered rows are written densely ("packed")
+ * in increasing y order, so {block_rows = 8, first_block = r, block_stride =
+ * N} is device r's share of an N-device interleaved tiling and {8, 0, 1} is
+ * the whole frame; runs give devices unequal shares (the multi-device frame
  * driver gives rank 0, which also assembles the frame, fewer rows:
- * {8, 0, P, 0, a} for it and {8, a + b (r - 1), P, 0, b} for rank r >= 1,
- * P = a + b (N - 1)).                                                        */
+ * {8, 0, P, 0, a, 1} for it and {8, a + r - 1, P, 0, b, N - 1} for rank
+ * r >= 1, P = a + b (N - 1): the peers' blocks interleave inside the period,
+ * so a frame whose block count is not a multiple of P gives its last partial
+ * period's blocks to distinct ranks).                                        */
 typedef struct {
   int32_t block_rows;
   int32_t first_block;
   int32_t block_stride;
   int32_t flags;      /* sdf_tiling_flags (0: packed rows) */
-  int32_t block_run;  /* consecutive blocks per period (0 or 1: one; <= block_stride) */
+  int32_t block_run;  /* blocks per period (0 or 1: one) */
+  int32_t run_step;   /* blocks between a run's blocks (0 or 1: consecutive);
+                         (run - 1) * step < block_stride */
 } sdf_tiling;
 
 /* SDF_TILING_FRAME_ROWS: write the owned rows at their frame positions (the
@@ -290,9 +295,9 @@ typedef enum { SDF_TILING_FRAME_ROWS = 1 } sdf_tiling_flags;
 /* ---- entry points -------------------------------------------------------- */
 
 /* The packed tiling of `rank`'s share of a `world`-device frame: rank 0
- * share_root blocks and every other rank share_peer blocks per period of
- * share_root + share_peer * (world - 1) 8-row blocks (1:1 = plain
- * interleave; world 1 = the whole frame). */
+ * share_root consecutive blocks and every other rank share_peer blocks,
+ * world - 1 apart, per period of share_root + share_peer * (world - 1)
+ * 8-row blocks (1:1 = plain interleave; world 1 = the whole frame). */
 int sdf_share_tiling(int32_t rank, int32_t world, int32_t share_root, int32_t share_peer,
                      sdf_tiling* tiling);
 

@@ -327,8 +327,11 @@ static void FN(render_rows)(const sdf_scene* s, const sdf_light* li,
   for (int pr = 0; pr < rows; pr++) {
     /* period blk, row `within` of its run of blocks (sdf_abi.h sdf_tiling) */
     int run = t->block_run > 1 ? t->block_run : 1;
+    int step = t->run_step > 1 ? t->run_step : 1;
     int blk = pr / (run * t->block_rows), within = pr % (run * t->block_rows);
-    int y = (t->first_block + blk * t->block_stride) * t->block_rows + within;
+    int j = within / t->block_rows;   /* the run's j-th block, step blocks apart */
+    int y = (t->first_block + blk * t->block_stride + j * step) * t->block_rows +
+            within % t->block_rows;
     (void)H;
     /* quad.y = (2y+1)/H - 1 (voxel_geometry.geom:26-52 + GL raster). */
     float qy = (float)(2 * y + 1) / (float)H - 1.0f;

@@ -112,14 +112,18 @@ static int make_uniforms(const sdf_camera* c, const sdf_params* p, oracle_unifor
 
 static int owned_rows(int height, const sdf_tiling* t) {
   int run = t->block_run > 1 ? t->block_run : 1;
+  int step = t->run_step > 1 ? t->run_step : 1;
   if (t->block_rows <= 0 || t->block_stride <= 0 || t->first_block < 0 || t->block_run < 0 ||
-      run > t->block_stride)
+      t->run_step < 0 || (long long)(run - 1) * step >= t->block_stride ||
+      (step > 1 && t->block_rows % 8 != 0))
     return SDF_E_INVALID_ARG;
   int nblocks = (height + t->block_rows - 1) / t->block_rows;
   int rows = 0;
-  /* blocks b >= first_block with (b - first_block) % block_stride < run */
+  /* blocks b >= first_block whose offset o = (b - first_block) % block_stride
+     in the period is a multiple of step below run * step */
   for (int b = t->first_block; b < nblocks; b++) {
-    if ((b - t->first_block) % t->block_stride >= run) continue;
+    int o = (b - t->first_block) % t->block_stride;
+    if (o % step != 0 || o / step >= run) continue;
     int r = height - b * t->block_rows;
     rows += r < t->block_rows ? r : t->block_rows;
   }
@@ -196,7 +200,7 @@ static int render(int twin, const sdf_scene* s, const sdf_camera* c, const sdf_l
                   float* rgba, int* steps, int nthreads) {
   if (!s || !c || !l || !m || !p || !rgba) return SDF_E_INVALID_ARG;
   if (p->width <= 0 || p->height <= 0) return SDF_E_INVALID_ARG;
-  sdf_tiling whole = {8, 0, 1, 0, 1};
+  sdf_tiling whole = {8, 0, 1, 0, 1, 1};
   const sdf_tiling* t = tiling ? tiling : &whole;
   int rows = owned_rows(p->height, t);
   if (rows < 0) return rows;

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 5
+SDF_ABI_VERSION = 6
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -90,7 +90,7 @@ class sdf_params(C.Structure):
 class sdf_tiling(C.Structure):
     _fields_ = [("block_rows", C.c_int32), ("first_block", C.c_int32),
                 ("block_stride", C.c_int32), ("flags", C.c_int32),
-                ("block_run", C.c_int32)]
+                ("block_run", C.c_int32), ("run_step", C.c_int32)]
 
 
 class sdf_driver_config(C.Structure):
@@ -101,7 +101,7 @@ class sdf_driver_config(C.Structure):
 
 STRUCT_SIZES = {
     "sdf_primitive": 64, "sdf_scene": 8 + 64 * SDF_MAX_PRIMS + 32, "sdf_camera": 88,
-    "sdf_light": 32, "sdf_material": 40, "sdf_params": 80, "sdf_tiling": 20,
+    "sdf_light": 32, "sdf_material": 40, "sdf_params": 80, "sdf_tiling": 24,
     "sdf_driver_config": 32,
 }
 

@@ -444,6 +444,7 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
       d->decode.block_stride[r] = t.block_stride;
       d->decode.block_rows[r] = t.block_rows;
       d->decode.chunk_rows[r] = t.block_rows * sdf::tiling_run(t);
+      d->decode.run_gap_rows[r] = sdf::tiling_gap_rows(t);
     }
   }
   if (rc == SDF_OK) rc = hip_ok(hipDeviceSynchronize());  // memsets done

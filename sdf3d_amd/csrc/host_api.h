@@ -27,6 +27,8 @@ struct RenderPlan {
 // Rows a tiling owns (sdf_owned_rows), or SDF_E_INVALID_ARG.
 int count_rows(int height, const sdf_tiling& t);
 int tiling_run(const sdf_tiling& t);
+int tiling_step(const sdf_tiling& t);
+int tiling_gap_rows(const sdf_tiling& t);  // (step - 1) * block_rows
 
 // Validate and prepare (tiling NULL = the whole frame).  SDF_OK or an SDF_E_*.
 int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,

@@ -46,6 +46,7 @@ struct KernelArgs {
   // tiling
   int32_t block_rows, first_block, block_stride, rows;
   int32_t chunk_rows;   // block_rows * run: rows of one period's run of blocks
+  int32_t run_gap_rows; // (run_step - 1) * block_rows: rows skipped between a run's blocks
   int32_t frame_rows;   // SDF_TILING_FRAME_ROWS: output row = frame row y
   // scene
   int32_t scene_kind, prim_count;
@@ -82,7 +83,7 @@ struct DecodeParts {
   long long part_stride;
   int rows[SDF_MAX_DECODE_PARTS], first_block[SDF_MAX_DECODE_PARTS],
       block_stride[SDF_MAX_DECODE_PARTS], block_rows[SDF_MAX_DECODE_PARTS],
-      chunk_rows[SDF_MAX_DECODE_PARTS];
+      chunk_rows[SDF_MAX_DECODE_PARTS], run_gap_rows[SDF_MAX_DECODE_PARTS];
 };
 int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, void* stream);
 

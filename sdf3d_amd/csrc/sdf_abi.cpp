@@ -25,23 +25,32 @@ static_assert(sizeof(sdf_camera) == 88, "sdf_camera layout");
 static_assert(sizeof(sdf_light) == 32, "sdf_light layout");
 static_assert(sizeof(sdf_material) == 40, "sdf_material layout");
 static_assert(sizeof(sdf_params) == 80, "sdf_params layout");
-static_assert(sizeof(sdf_tiling) == 20, "sdf_tiling layout");
+static_assert(sizeof(sdf_tiling) == 24, "sdf_tiling layout");
 static_assert(sizeof(sdf_driver_config) == 32, "sdf_driver_config layout");
 
 namespace sdf {
 
 int tiling_run(const sdf_tiling& t) { return t.block_run > 1 ? t.block_run : 1; }
+int tiling_step(const sdf_tiling& t) { return t.run_step > 1 ? t.run_step : 1; }
+int tiling_gap_rows(const sdf_tiling& t) { return (tiling_step(t) - 1) * t.block_rows; }
 
 int count_rows(int height, const sdf_tiling& t) {
   if (t.block_rows <= 0 || t.block_stride <= 0 || t.first_block < 0 || height < 0 ||
-      t.block_run < 0 || tiling_run(t) > t.block_stride ||
+      t.block_run < 0 || t.run_step < 0 ||
+      (long long)(tiling_run(t) - 1) * tiling_step(t) >= t.block_stride ||
       (t.flags & ~SDF_TILING_FRAME_ROWS) != 0)
     return SDF_E_INVALID_ARG;
+  // spaced runs keep every 8-row tile of packed rows inside one block (the
+  // kernels then find a tile's block once per wave)
+  if (tiling_step(t) > 1 && t.block_rows % 8 != 0) return SDF_E_INVALID_ARG;
   // every period contributes its run of blocks, cut at the frame's last row
   long long rows = 0;
   const long long B = t.block_rows;
-  for (long long b = t.first_block; b * B < height; b += t.block_stride)
-    rows += std::min<long long>((b + tiling_run(t)) * B, height) - b * B;
+  for (long long b0 = t.first_block; b0 * B < height; b0 += t.block_stride)
+    for (long long j = 0; j < tiling_run(t); ++j) {
+      const long long b = b0 + j * tiling_step(t);
+      if (b * B < height) rows += std::min<long long>((b + 1) * B, height) - b * B;
+    }
   return (int)rows;
 }
 
@@ -100,7 +109,7 @@ bool finite3(const float* v) {
 int run_of(const sdf_tiling& t) { return sdf::tiling_run(t); }
 using sdf::count_rows;
 
-const sdf_tiling kWholeFrame = {8, 0, 1, 0, 1};
+const sdf_tiling kWholeFrame = {8, 0, 1, 0, 1, 1};
 
 // Per-frame preparation of the primitive parameter blocks the kernels read
 // (layouts in render_kernel.inc).  Every derived value is computed in fp32
@@ -303,6 +312,7 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
   a.inv_height = 1.0f / (float)params->height;
   a.block_rows = t.block_rows;
   a.chunk_rows = t.block_rows * run_of(t);
+  a.run_gap_rows = sdf::tiling_gap_rows(t);
   a.first_block = t.first_block;
   a.block_stride = t.block_stride;
   a.rows = rows;
@@ -426,8 +436,10 @@ int sdf_share_tiling(int32_t rank, int32_t world, int32_t share_root, int32_t sh
   if (world == 1) {
     *tiling = kWholeFrame;
   } else {
-    *tiling = sdf_tiling{8, rank == 0 ? 0 : a + b * (rank - 1), a + b * (world - 1), 0,
-                         rank == 0 ? a : b};
+    // peers' blocks interleave (world - 1 apart), so the frame's last partial
+    // period spreads over distinct ranks instead of one peer's whole run
+    *tiling = sdf_tiling{8, rank == 0 ? 0 : a + rank - 1, a + b * (world - 1), 0,
+                         rank == 0 ? a : b, rank == 0 || b == 1 ? 1 : world - 1};
   }
   return SDF_OK;
 }
@@ -545,6 +557,7 @@ int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_str
     d.block_stride[r] = t.block_stride;
     d.block_rows[r] = t.block_rows;
     d.chunk_rows[r] = t.block_rows * run_of(t);
+    d.run_gap_rows[r] = sdf::tiling_gap_rows(t);
   }
   const int err = sdf::launch_tiles_decode(d, frame, parts, stream);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;

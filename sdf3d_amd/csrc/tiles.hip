@@ -110,8 +110,12 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
   // 8 ty at row `within` of its run of blocks (sdf_tiling)
   const int chunk = D.chunk_rows[part];
   const int first_blk = D.first_block[part], period = D.block_stride[part], brows = D.block_rows[part];
+  const int gap = D.run_gap_rows[part];
   int ty = tbase / tiles_x, tx = tbase - ty * tiles_x;
   int blk = (8 * ty) / chunk, within = 8 * ty - blk * chunk;
+  // spaced runs (gap > 0, block_rows % 8 == 0): the tile's block of its run
+  // is jb, and its row in that block wb, stepped with `within`
+  int jb = gap ? within / brows : 0, wb = within - jb * brows;
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
     if (k >= nt) continue;
@@ -119,9 +123,16 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
       tx = 0;
       ++ty;
       within += 8;
+      wb += 8;
+      if (wb >= brows) {
+        wb -= brows;
+        ++jb;
+      }
       while (within >= chunk) {
         within -= chunk;
         ++blk;
+        jb = 0;
+        wb = within;
       }
     }
     const uint32_t head = __builtin_amdgcn_readlane((int)hdv.x, k);
@@ -218,7 +229,7 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
         w -= chunk;
         ++b;
       }
-      const int y = (first_blk + b * period) * brows + w;
+      const int y = (first_blk + b * period) * brows + w + jb * gap;
       frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
     }
     (void)nq;

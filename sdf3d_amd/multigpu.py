@@ -52,22 +52,26 @@ from typing import Callable, Optional
 import numpy as np
 
 
-def share_blocks(rank: int, world: int, shares=(1, 1)) -> tuple[int, int, int]:
-    """(first block, run, period) of `rank` in the tiling with shares (a, b):
-    per period of P = a + b (world - 1) blocks rank 0 owns the first a, rank
-    r >= 1 the b from a + b (r - 1) on (renderer.tiling, sdf_tiling)."""
+def share_blocks(rank: int, world: int, shares=(1, 1)) -> tuple[int, int, int, int]:
+    """(first block, run, period, step) of `rank` in the tiling with shares
+    (a, b): per period of P = a + b (world - 1) blocks rank 0 owns the first
+    a, rank r >= 1 the b blocks a + r - 1 + j (world - 1), j < b, interleaved
+    with the other peers' (renderer.tiling, sdf_tiling.run_step)."""
     a, b = shares
     period = a + b * (world - 1)
-    return (0, a, period) if rank == 0 else (a + b * (rank - 1), b, period)
+    if rank == 0:
+        return (0, a, period, 1)
+    return (a + rank - 1, b, period, world - 1 if b > 1 else 1)
 
 
 def owned_row_ids(height: int, rank: int, world: int, block_rows: int = 8,
                   shares=(1, 1)) -> np.ndarray:
     """Frame rows (y) owned by `rank`, in packed order."""
-    first, run, period = share_blocks(rank, world, shares)
+    first, run, period, step = share_blocks(rank, world, shares)
     y = np.arange(height)
     b = y // block_rows
-    return y[(b >= first) & ((b - first) % period < run)]
+    o = (b - first) % period
+    return y[(b >= first) & (o % step == 0) & (o // step < run)]
 
 
 def owned_rows_py(height: int, rank: int, world: int, block_rows: int = 8,

@@ -19,8 +19,10 @@ def tiling(rank: int = 0, world: int = 1, block_rows: int = 8,
     """Interleaved row-block tiling of `world` devices.
 
     shares = (a, b): per period of P = a + b (world - 1) blocks, rank 0 owns
-    the first a blocks and rank r >= 1 the b blocks from a + b (r - 1) on
-    ((1, 1): device r owns blocks r, r + world, ...).  frame_rows: write the
+    the first a blocks and rank r >= 1 the b blocks a + r - 1 + j (world - 1),
+    j < b, interleaved with the other peers' (so a frame whose block count is
+    not a multiple of P gives the last partial period to distinct ranks;
+    (1, 1): device r owns blocks r, r + world, ...).  frame_rows: write the
     rows at their frame positions of a full-height buffer
     (SDF_TILING_FRAME_ROWS)."""
     a, b = shares
@@ -29,8 +31,9 @@ def tiling(rank: int = 0, world: int = 1, block_rows: int = 8,
     t = abi.sdf_tiling()
     t.block_rows = block_rows
     t.block_stride = a + b * (world - 1)
-    t.first_block = 0 if rank == 0 else a + b * (rank - 1)
+    t.first_block = 0 if rank == 0 else a + rank - 1
     t.block_run = a if rank == 0 else b
+    t.run_step = 1 if rank == 0 or b == 1 else world - 1
     t.flags = abi.TILING_FRAME_ROWS if frame_rows else 0
     return t
 

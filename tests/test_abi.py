@@ -162,18 +162,20 @@ def test_owned_rows_matches_oracle_and_partitions(height, world):
 def tiling_rows(height, t):
     """Frame rows a tiling owns, in packed order, straight from the
     definition in include/sdf_abi.h (sdf_tiling)."""
-    run = max(t.block_run, 1)
+    run, step = max(t.block_run, 1), max(t.run_step, 1)
     return [y for y in range(height)
             if y // t.block_rows >= t.first_block
-            and (y // t.block_rows - t.first_block) % t.block_stride < run]
+            and (y // t.block_rows - t.first_block) % t.block_stride % step == 0
+            and (y // t.block_rows - t.first_block) % t.block_stride // step < run]
 
 
 @pytest.mark.parametrize("height", [1, 9, 71, 270, 1080, 2160])
 @pytest.mark.parametrize("world,shares", [(2, (1, 2)), (3, (2, 3)), (4, (3, 1)), (8, (1, 2)),
                                           (8, (1, 3)), (8, (2, 5))])
 def test_weighted_tiling_partitions_frame(height, world, shares):
-    """Unequal shares (sdf_tiling.block_run): every rank's rows as the
-    library and the oracle count them, and together exactly the frame."""
+    """Unequal shares (sdf_tiling.block_run, peers' runs spaced by
+    run_step): every rank's rows as the library and the oracle count them,
+    and together exactly the frame."""
     rows = []
     for r in range(world):
         t = renderer.tiling(r, world, 8, shares=shares)
@@ -203,6 +205,17 @@ def test_tiling_run_validation():
     assert lib.sdf_owned_rows(100, C.byref(t)) == n0 == len(tiling_rows(100, t))
     with pytest.raises(ValueError):
         renderer.tiling(0, 2, 8, shares=(0, 1))
+    # spaced runs: the run must fit its period, and blocks hold whole 8-row tiles
+    t = renderer.tiling(1, 8, 8, shares=(1, 3))
+    assert (t.block_run, t.run_step, t.block_stride) == (3, 7, 22)
+    t.run_step = 11                           # (3 - 1) * 11 = 22: past the period
+    assert lib.sdf_owned_rows(100, C.byref(t)) == abi.SDF_E_INVALID_ARG
+    t.run_step = -1
+    assert lib.sdf_owned_rows(100, C.byref(t)) == abi.SDF_E_INVALID_ARG
+    t.run_step, t.block_rows = 7, 4
+    assert lib.sdf_owned_rows(100, C.byref(t)) == abi.SDF_E_INVALID_ARG
+    t.run_step = 1                            # consecutive runs take any block size
+    assert lib.sdf_owned_rows(100, C.byref(t)) == len(tiling_rows(100, t))
 
 
 def test_strerror():

@@ -168,8 +168,9 @@ def test_tiling_and_deinterleave_reassemble_frame(renderer, world):
 
 @pytest.mark.parametrize("world,shares", [(3, (1, 2)), (8, (1, 3))])
 def test_weighted_tiling_renders_its_rows(renderer, world, shares):
-    """Runs of blocks (sdf_tiling.block_run): each rank's packed rows are the
-    whole frame's rows it owns, bit for bit, and the oracle agrees on one."""
+    """Runs of blocks (sdf_tiling.block_run, spaced by run_step): each
+    rank's packed rows are the whole frame's rows it owns, bit for bit, and
+    the oracle agrees on one."""
     import torch
     f = scenes.config("C3", 320, 183, precision=abi.PRECISION_FAST, pose=2)
     whole, _ = renderer.render(f)
@@ -177,9 +178,10 @@ def test_weighted_tiling_renders_its_rows(renderer, world, shares):
     H = f.params.height
     for r in range(world):
         t = R.tiling(r, world, 8, shares=shares)
-        run = max(t.block_run, 1)
+        run, step = max(t.block_run, 1), max(t.run_step, 1)
         ys = [y for y in range(H) if y // 8 >= t.first_block
-              and (y // 8 - t.first_block) % t.block_stride < run]
+              and (y // 8 - t.first_block) % t.block_stride % step == 0
+              and (y // 8 - t.first_block) % t.block_stride // step < run]
         part, _ = renderer.render(f, t)
         torch.cuda.synchronize()
         assert part.shape[0] == len(ys)

@@ -171,7 +171,7 @@ def test_lag_bound():
 
 
 @pytest.mark.parametrize("world,shares", [(1, (1, 1)), (2, (4, 3)), (4, (1, 1)), (8, (1, 2)),
-                                          (5, (3, 2))])
+                                          (5, (3, 2)), (8, (1, 3)), (4, (3, 4))])
 def test_native_driver_tilings_match(world, shares):
     """The native driver's shares (sdf_share_tiling) are the Python driver's."""
     import ctypes as C
@@ -184,7 +184,21 @@ def test_native_driver_tilings_match(world, shares):
         for H in (43, 2160):
             assert R.owned_rows(H, t) == R.owned_rows(H, want) == owned_rows_py(H, r, world, 8, shares)
         if world > 1:
-            assert (t.block_rows, t.first_block, t.block_stride, t.block_run) == \
-                (want.block_rows, want.first_block, want.block_stride, want.block_run)
+            assert (t.block_rows, t.first_block, t.block_stride, t.block_run, t.run_step) == \
+                (want.block_rows, want.first_block, want.block_stride, want.block_run,
+                 want.run_step)
     bad = abi.sdf_tiling()
     assert lib.sdf_share_tiling(world, world, 1, 1, C.byref(bad)) == abi.SDF_E_INVALID_ARG
+
+
+@pytest.mark.parametrize("world,shares,busiest", [(8, (1, 3), 296), (4, (3, 4), 576),
+                                                  (2, (1, 1), 1080)])
+def test_share_rows_balanced_on_4k(world, shares, busiest):
+    """The peers' interleaved runs (sdf_tiling.run_step) spread a 4K frame's
+    last partial period over distinct ranks: at N = 8, 1:3 (270 blocks,
+    period 22) no peer owns more than 37 blocks (consecutive runs gave one
+    peer 39, 312 rows), and the rows still partition the frame."""
+    rows = [R.owned_rows(2160, R.tiling(r, world, 8, shares=shares)) for r in range(world)]
+    assert sum(rows) == 2160 and max(rows[1:]) == busiest
+    ids = np.concatenate([owned_row_ids(2160, r, world, 8, shares) for r in range(world)])
+    assert np.array_equal(np.sort(ids), np.arange(2160))
