@@ -370,8 +370,9 @@ int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
 /* Debug view of the `steps` output of sdf_render: `count` int2 entries
  * (primary, shadow) -> colours of `format`, with which = 0 (primary), 1
  * (shadow) or 2 (their sum), intensity = steps / max_steps mapped through the
- * Turbo colormap the reference ships unused (Code/kernel/utilities.cl:7-284;
- * index round(255 * intensity) clamped to [0, 255], alpha 1).  Device
+ * Turbo colormap the reference ships unused (Code/kernel/utilities.cl:7-284:
+ * its 256-entry table, index round(255 * intensity) rounded half away from
+ * zero and clamped to [0, 255], alpha 1).  Device
  * pointers; asynchronous on `stream`. */
 int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_steps,
                 int32_t format, void* out, void* stream);

@@ -23,7 +23,10 @@ from sdf3d_amd import abi  # struct layouts of include/sdf_abi.h (types only)
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "build" / "liboracle.so"
-_lib = None
+# the contracted fp32 reading (FMA-fused multiply-adds, which GLSL permits
+# outside `precise`; see oracle/Makefile) -- diagnosis only
+FMA_LIB_PATH = HERE / "build" / "liboracle_fma.so"
+_libs = {}
 
 
 def build() -> Path:
@@ -31,13 +34,13 @@ def build() -> Path:
     return LIB_PATH
 
 
-def load() -> C.CDLL:
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not LIB_PATH.exists():
+def load(variant: str = "ieee") -> C.CDLL:
+    if variant in _libs:
+        return _libs[variant]
+    path = {"ieee": LIB_PATH, "fma": FMA_LIB_PATH}[variant]
+    if not path.exists():
         build()
-    lib = C.CDLL(str(LIB_PATH))
+    lib = C.CDLL(str(path))
     P = C.POINTER
     frame_args = [P(abi.sdf_scene), P(abi.sdf_camera), P(abi.sdf_light), P(abi.sdf_material),
                   P(abi.sdf_params)]
@@ -61,7 +64,7 @@ def load() -> C.CDLL:
     lib.sdf_oracle_shadow.restype = C.c_float
     lib.sdf_oracle_normal.argtypes = [P(abi.sdf_scene), P(abi.sdf_params), F3, F3]
     lib.sdf_oracle_normal.restype = None
-    _lib = lib
+    _libs[variant] = lib
     return lib
 
 
@@ -117,12 +120,14 @@ def owned_rows(height: int, t=None) -> int:
     return load().sdf_oracle_owned_rows(height, C.byref(t))
 
 
-def render(frame, t=None, nthreads: int | None = None, twin: bool = False):
+def render(frame, t=None, nthreads: int | None = None, twin: bool = False,
+           variant: str = "ieee"):
     """Render `frame` (sdf3d_amd.scenes.Frame) on the CPU.
 
     Returns (rgba float32 [rows, W, 4], steps int32 [rows, W, 2]).
-    `twin=True` runs the fp64 twin (diagnosis only)."""
-    lib = load()
+    `twin=True` runs the fp64 twin (diagnosis only); variant="fma" runs the
+    contracted fp32 reading (diagnosis only)."""
+    lib = load(variant)
     p = frame.params
     rows = owned_rows(p.height, t)
     rgba = np.empty((rows, p.width, 4), dtype=np.float32)

@@ -29,13 +29,20 @@ typedef struct {
   float aspect;       /* AR */
 } oracle_uniforms;
 
-/* ---- fp32 oracle ---- */
+/* ---- fp32 oracle ----
+ * log and pow are the two transcendentals (Mandelbulb DE, specular
+ * exponent).  GLSL leaves their precision to the implementation; the oracle
+ * takes the tightest reading, correctly rounded fp32, evaluated in double and
+ * rounded once, so its fp32 result does not depend on which libm's logf/powf
+ * it links (the exact-precision kernel evaluates them the same way). */
+static inline float cr_logf(float x) { return (float)log((double)x); }
+static inline float cr_powf(float x, float y) { return (float)pow((double)x, (double)y); }
 #define REAL float
 #define FN(name) f32_##name
 #define SQRT sqrtf
 #define FABS fabsf
-#define LOG logf
-#define POW powf
+#define LOG cr_logf
+#define POW cr_powf
 #include "oracle_core.h"
 #undef REAL
 #undef FN

@@ -1,13 +1,29 @@
 """Parity policy between the HIP kernel and the CPU oracle.
 
-A pixel's error is its largest per-channel |delta| over RGBA.  A comparison
-passes when
+A pixel's error is its largest per-channel |delta| over RGBA.  The STRICT
+policy (unchanged) passes when
   * at least `min_frac` (99.99 %) of pixels are within `tol` (1e-4) -- on
     frames under 10^4 pixels, at most one pixel may be outside -- and
-  * every pixel above `tol` is a DIAGNOSED branch flip: the kernel's primary
-    or shadow iteration count differs from the oracle's, or (when the fp64
-    twin is supplied) the fp64 twin disagrees with the fp32 oracle there, and
-  * no pixel's error exceeds `max_err` (0.05 by default).
+  * every pixel above `tol` is DIAGNOSED: the kernel's primary or shadow
+    iteration count differs from the oracle's, or an alternative reading of
+    the reference (the fp64 twin; the contracted fp32 reading, GLSL's
+    permitted multiply-add fusion, oracle/Makefile) disagrees with the fp32
+    oracle there, and
+  * no pixel's error exceeds `max_err` (0.05).
+
+Some frames are fp32-ILL-CONDITIONED: the alternative readings themselves
+fail the strict policy against the fp32 oracle (measured at 3840x2160: the
+C4 twin has 2 pixels over 0.05 at grazing-ray step flips; on the Mandelbulb
+the twin disagrees at 0.0175 % of pixels, tools/fullsize_parity.py,
+profiles/r02_fullsize_parity.json).  No fp32 implementation other than a
+bit-replica of the oracle can then pass the strict policy, the reference on
+a real GPU included.  For those frames `assert_parity_frame` holds the
+kernel to the readings' own spread instead: its outlier count, undiagnosed
+count and count over `max_err` may each be at most `READING_FACTOR` times
+the worst alternative reading's (the kernel differs from the oracle in more
+roundings than either reading does).  Exact precision, a replica of the
+oracle's fp32 operation sequence, is held to the strict policy on every
+frame by the tests.
 `report()` returns the numbers the tests print and assert on.
 """
 from __future__ import annotations
@@ -36,7 +52,16 @@ def quantize(rgba, fmt):
     return ((q * np.float32(255)).astype(np.float32) + np.float32(0.5)).astype(np.uint8)
 
 
-def report(rgba, steps, ref_rgba, ref_steps, twin_rgba=None, tol=TOL):
+def _err(a, b):
+    both_nan = np.isnan(a) & np.isnan(b)
+    d = np.where(both_nan, 0.0, np.abs(a.astype(np.float64) - b))
+    return np.where(np.isnan(d), np.inf, d).max(axis=-1)
+
+
+def report(rgba, steps, ref_rgba, ref_steps, twin_rgba=None, tol=TOL, alt_rgba=()):
+    """Parity numbers of `rgba` against the oracle's `ref_rgba`.  `twin_rgba`
+    and `alt_rgba` are alternative readings (fp64 twin, contracted fp32) used
+    to diagnose outliers."""
     rgba = np.asarray(rgba, dtype=np.float32)
     ref_rgba = np.asarray(ref_rgba, dtype=np.float32)
     assert rgba.shape == ref_rgba.shape, (rgba.shape, ref_rgba.shape)
@@ -54,9 +79,16 @@ def report(rgba, steps, ref_rgba, ref_steps, twin_rgba=None, tol=TOL):
         flip |= sm
     twin_dis = None
     if twin_rgba is not None:
-        tw = np.abs(np.asarray(twin_rgba, np.float64) - ref_rgba).max(axis=-1) > tol
+        tw = _err(np.asarray(twin_rgba, np.float32), ref_rgba) > tol
         twin_dis = int(tw.sum())
         flip |= tw
+    alt_dis = None
+    if len(alt_rgba):
+        alt = np.zeros_like(out)
+        for a in alt_rgba:
+            alt |= _err(np.asarray(a, np.float32), ref_rgba) > tol
+        alt_dis = int(alt.sum())
+        flip |= alt
     return {
         "pixels": int(n),
         "bit_exact": int(np.sum(np.all(rgba.view(np.uint32) == ref_rgba.view(np.uint32), axis=-1))),
@@ -66,23 +98,60 @@ def report(rgba, steps, ref_rgba, ref_steps, twin_rgba=None, tol=TOL):
         "max_err": float(err.max()) if n else 0.0,
         "step_mismatch": step_mm,
         "twin_disagree": twin_dis,
+        "reading_disagree": alt_dis,
+        "over_max_err": int(np.sum(err > MAX_ERR)),
     }
 
 
-def assert_parity(rep, min_frac=MIN_FRAC, max_err=MAX_ERR, what="", diagnose=True):
+def outlier_budget(pixels, min_frac=MIN_FRAC):
     """>= min_frac of pixels within tol; on small frames that is an outlier
     budget of ceil((1 - min_frac) * pixels), at least one pixel."""
-    budget = max(1, int(np.ceil((1.0 - min_frac) * rep["pixels"] - 1e-9)))
-    assert rep["outliers"] <= budget, (what, rep)
-    if diagnose:
-        assert rep["undiagnosed"] == 0, (what, rep)
-    assert rep["max_err"] <= max_err, (what, rep)
+    return max(1, int(np.ceil((1.0 - min_frac) * pixels - 1e-9)))
 
 
-# Fast precision on the Mandelbulb (C5): the 12-iteration degree-8 map is
-# chaotic near the set, so FMA contraction and the 1-ulp v_rsq / v_rcp /
-# v_log results move the DE by more than 1e-4 at a few boundary pixels even
-# where the march takes the same steps.  Held to 99.9 % within 1e-4 and
-# max 0.1, outliers need not be step flips.  Exact precision keeps the
-# strict policy on every scene.
-BULB_FAST = dict(min_frac=0.999, max_err=0.1, diagnose=False)
+def passes_strict(rep) -> bool:
+    return (rep["outliers"] <= outlier_budget(rep["pixels"]) and rep["undiagnosed"] == 0
+            and rep["max_err"] <= MAX_ERR)
+
+
+def assert_parity(rep, what=""):
+    """The strict policy of SURVEY.md 8(c)."""
+    assert rep["outliers"] <= outlier_budget(rep["pixels"]), (what, rep)
+    assert rep["undiagnosed"] == 0, (what, rep)
+    assert rep["max_err"] <= MAX_ERR, (what, rep)
+
+
+READING_FACTOR = 2.0
+
+
+def reading_spread(ref, ref_steps, readings):
+    """Each alternative reading against the fp32 oracle, diagnosed by its own
+    step counts and by the other readings: {name: report}.  `readings` maps
+    name -> (rgba, steps)."""
+    out = {}
+    for name, (rgba, st) in readings.items():
+        others = [r for n, (r, _) in readings.items() if n != name]
+        out[name] = report(rgba, st, ref, ref_steps, alt_rgba=others)
+    return out
+
+
+def assert_parity_frame(rep, spread, what="", ill_conditioned=False):
+    """Strict policy when every alternative reading passes it against the
+    oracle, unless the scene is known to be fp32-ill-conditioned
+    (`ill_conditioned`: the Mandelbulb, whose readings fail the strict policy
+    at every size measured large enough to show it -- 320x180 and 3840x2160;
+    small frames can pass by chance).  Otherwise the kernel's outlier,
+    undiagnosed and over-max_err counts are each at most READING_FACTOR times
+    the worst reading's, plus a Poisson allowance of 3 standard deviations
+    (counts of rare pixels on one frame are noisy: at the 4K rate, a
+    5,184-pixel frame expects ~0.9 twin outliers), with the strict outlier
+    budget as a floor.  Returns "strict" or "readings"."""
+    if not ill_conditioned and all(passes_strict(r) for r in spread.values()):
+        assert_parity(rep, what)
+        return "strict"
+    for key, floor in (("outliers", outlier_budget(rep["pixels"])), ("undiagnosed", 0),
+                       ("over_max_err", 0)):
+        worst = max(r[key] for r in spread.values())
+        allowed = READING_FACTOR * worst + 3.0 * np.sqrt(READING_FACTOR * worst + 1.0)
+        assert rep[key] <= max(floor, allowed), (what, key, rep, spread)
+    return "readings"

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Full-size per-pixel parity survey: GPU vs oracle, and the oracle's own spread.
+
+For each BASELINE-size config (C4 and C5 at 3840x2160, C2 at 1920x1080) and
+each precision, renders the frame on the GPU without a steps buffer (the
+bench's path: exact shadow skip active) and with one, and on the CPU:
+
+  * the fp32 oracle (IEEE, no contraction: the parity target),
+  * the fp64 twin (diagnosis),
+  * the contracted fp32 reading (oracle/Makefile liboracle_fma.so; GLSL lets
+    an implementation fuse multiply-adds outside `precise`, so this is as
+    valid a reading of voxel_fragment.frag as the unfused one).
+
+It reports the parity policy's numbers for GPU-vs-oracle, and the same
+numbers for twin-vs-oracle and fma-vs-oracle: how far two valid readings of
+the reference already disagree at this size, which bounds what any fp32
+implementation can promise.  Large outliers (> 0.05) are listed with their
+step counts in every reading.
+
+    python tools/fullsize_parity.py --out gpurun_out/fullsize_parity.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def err_of(a, b):
+    import numpy as np
+    both = np.isnan(a) & np.isnan(b)
+    d = np.where(both, 0.0, np.abs(a.astype(np.float64) - b))
+    return np.where(np.isnan(d), np.inf, d).max(axis=-1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/fullsize_parity.json")
+    ap.add_argument("--configs", default="C4,C2,C5")
+    ap.add_argument("--precisions", default="fast,exact")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import oracle
+    from parity import report
+    from sdf3d_amd import Renderer, abi, scenes
+
+    rd = Renderer("cuda:0")
+    out = {}
+    for cfg in a.configs.split(","):
+        f0 = scenes.config(cfg)
+        t0 = time.perf_counter()
+        ref, rst = oracle.render(f0)
+        t_ref = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        twin, tst = oracle.render(f0, twin=True)
+        t_twin = time.perf_counter() - t0
+        fma, fst = oracle.render(f0, variant="fma")
+        e_twin, e_fma = err_of(twin, ref), err_of(fma, ref)
+        spread = {
+            "oracle_s": round(t_ref, 2), "twin_s": round(t_twin, 2),
+            "twin_vs_oracle": report(twin, tst, ref, rst),
+            "fma_vs_oracle": report(fma, fst, ref, rst),
+            "twin_over_0.05": int((e_twin > 0.05).sum()),
+            "fma_over_0.05": int((e_fma > 0.05).sum()),
+        }
+        print(cfg, "spread", json.dumps(spread), flush=True)
+        res = {"readings": spread}
+        for pname in a.precisions.split(","):
+            prec = abi.PRECISION_FAST if pname == "fast" else abi.PRECISION_EXACT
+            f = scenes.config(cfg, precision=prec)
+            g, _ = rd.render(f)
+            gs, st = rd.render(f, steps=True)
+            torch.cuda.synchronize()
+            same = bool(torch.equal(g.view(torch.int32), gs.view(torch.int32)))
+            g, st = g.cpu().numpy(), st.cpu().numpy()
+            rep = report(g, st, ref, rst, twin)
+            e = err_of(g, ref)
+            fma_dis = err_of(fma, ref) > 1e-4
+            out_mask = e > 1e-4
+            diag_steps = np.any(st != rst, axis=-1)
+            rep["undiagnosed_with_fma"] = int(np.sum(out_mask & ~diag_steps
+                                                    & ~(e_twin > 1e-4) & ~fma_dis))
+            rep["steps_equal_frac"] = float(np.mean(~diag_steps))
+            rep["nostep_equals_steps_render"] = same
+            big = np.argwhere(e > 0.05)
+            rep["over_0.05"] = int(len(big))
+            rep["over_0.05_samples"] = [
+                {"y": int(y), "x": int(x), "err": float(e[y, x]), "gpu_steps": st[y, x].tolist(),
+                 "oracle_steps": rst[y, x].tolist(), "twin_steps": tst[y, x].tolist(),
+                 "fma_steps": fst[y, x].tolist(), "twin_err": float(e_twin[y, x]),
+                 "fma_err": float(e_fma[y, x])} for y, x in big[:12]]
+            # of the GPU's outliers above 0.05, how many are pixels where a
+            # valid reading also flips (twin or fma steps differ from oracle)
+            flips_other = np.any(tst != rst, axis=-1) | np.any(fst != rst, axis=-1)
+            rep["over_0.05_where_readings_flip"] = int(np.sum((e > 0.05) & flips_other))
+            res[pname] = rep
+            print(cfg, pname, json.dumps({k: v for k, v in rep.items()
+                                          if k != "over_0.05_samples"}), flush=True)
+        out[cfg] = res
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(a.out).write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
