@@ -18,11 +18,12 @@ i+2 render.  Total work per step is one frame whatever N is ("scaling":
 
 Prints ONE JSON line (rank 0).  `value` = frame pixels x K / max-over-ranks
 wall time of the K timed steps, in Mpixels/s.  `roofline` is the render
-kernel's achieved algorithmic FP32 rate (SURVEY.md 8(d) counting rule,
-per-pixel step counts from the CPU oracle's full-frame statistics in
-tests/golden/stats_<cfg>_p0.npz) over the kernel's average duration measured
-with HIP events on the launch stream, against the 157.3 TFLOP/s FP32 vector
-peak.  `cpu_baseline` times the CPU oracle (a restatement of the reference
+kernel's executed FP32 rate (the hardware flop count of the committed PMC
+summary, profiles/pmc_<cfg>_<prec>.json) over the kernel's average duration
+measured with HIP events on the launch stream, against the 157.3 TFLOP/s FP32
+vector peak, with the counter-based VALU busy of the same PMC run and, as
+`alg_equiv`, the SURVEY.md 8(d) algorithmic count (oracle step counts in
+tests/golden/stats_<cfg>_p0.npz) over the same time (see roofline()).  `cpu_baseline` times the CPU oracle (a restatement of the reference
 shader: the reference's own OpenCL kernel is empty and no CPU OpenCL device
 exists) on a bounded sample of the same frame, rank 0 at N=1 only.
 """
@@ -122,6 +123,57 @@ def pmc_summary(cfg, precision):
         return json.loads(p.read_text())
     except Exception:
         return {}
+
+
+def valu_cycles_per_unit():
+    """gfx950 normalisation of SQ_ACTIVE_INST_VALU (tools/valu_busy_calib.py,
+    profiles/r02_valu_busy_calib.json): SIMD cycles per counter unit, from
+    kernels of pure full-rate VALU chains at full occupancy."""
+    try:
+        return float(json.loads((ROOT / "profiles" / "r02_valu_busy_calib.json")
+                                .read_text())["cycles_per_unit"])
+    except Exception:
+        return None
+
+
+def roofline(pmc, alg_flops, kavg_ms, store_bytes):
+    """The render kernel against the FP32 VALU roofline.
+
+    achieved = EXECUTED FP32 flops per launch -- the hardware count
+    64 * (ADD + MUL + TRANS + 2 FMA) wave-instructions from the committed
+    rocprofv3 PMC summary of the same kernel (profiles/pmc_<cfg>_<prec>.json,
+    tools/pmc_traffic.py) -- over the live kernel time; frac <= 1 by
+    construction.  valu_busy is the counter-based issue utilisation of the
+    same PMC run (SQ_ACTIVE_INST_VALU x the calibrated gfx950 cycles per
+    unit / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)); the counter counts a
+    half-rate min/max/cmp as one unit, so it is a lower bound (a v_min-only
+    chain reads 0.60).  alg_equiv is the SURVEY.md 8(d) counting rule (every
+    primitive at every step, oracle step counts): exact culling skips
+    evaluations that rule counts, so it can exceed the peak."""
+    roof = {"bound": "valu", "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": None, "traffic": pmc.get("hbm_bytes_per_launch"),
+            "kernel_ms": round(kavg_ms, 4),
+            "store_GBps": round(store_bytes / (kavg_ms * 1e-3) / 1e9, 1)}
+    ex = pmc.get("executed_flops_per_launch")
+    if ex:
+        ach = ex / (kavg_ms * 1e-3) / 1e12
+        roof.update(achieved=round(ach, 2), frac=round(ach / FP32_PEAK_TFLOPS, 4),
+                    executed_flops_per_launch=ex,
+                    basis="executed FP32 flops (PMC) / live kernel time")
+    c = pmc.get("counters", {})
+    cpu = valu_cycles_per_unit()
+    if cpu and c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
+        roof["valu_busy"] = round(cpu * c["SQ_ACTIVE_INST_VALU"]
+                                  / (1024 * c["GRBM_GUI_ACTIVE"] / 8), 4)
+    if alg_flops is not None:
+        alg = alg_flops / (kavg_ms * 1e-3) / 1e12
+        roof["alg_equiv"] = {"flops_per_launch": alg_flops, "TFLOPs": round(alg, 2),
+                             "frac": round(alg / FP32_PEAK_TFLOPS, 4),
+                             "note": "SURVEY 8(d) rule: every primitive at every step; "
+                                     "exact culling skips evaluations it counts"}
+    if roof["achieved"] is None and alg_flops is None:
+        return None
+    return roof
 
 
 def lib_bpp(frame):
@@ -443,33 +495,9 @@ def main():
             # for the GPU / peers excluded (native driver only)
             "driver_host_us_per_frame": drv.stats()["host_us_per_frame"] if native else None,
         }
-        if flops is not None:
-            ach = flops / (kavg_ms * 1e-3) / 1e12
-            pmc = (pmc_summary(args.config, args.precision)
-                   if world == 1 and args.format == "rgba32f" else {})
-            out["roofline"] = {"bound": "valu", "achieved": round(ach, 2),
-                               "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(ach / FP32_PEAK_TFLOPS, 4),
-                               "traffic": pmc.get("hbm_bytes_per_launch"),
-                               "flops_per_launch": flops,
-                               "store_GBps": round(rows * W * lib_bpp(frame) / (kavg_ms * 1e-3)
-                                                   / 1e9, 1)}
-            im = pmc.get("valu_issue_model")
-            if im:
-                # hardware view: the kernel's VALU issue cycles (instruction
-                # mix x measured issue cost) over its cycles, as a range
-                out["roofline"]["valu_issue_util"] = [round(x, 3) for x in im["util"]]
-            out["roofline"]["note"] = ("achieved counts every primitive at every step "
-                                       "(SURVEY 8(d) rule); exact culling skips provably "
-                                       "dead evaluations, so frac can exceed 1")
-            ex = pmc.get("executed_flops_per_launch")
-            if ex:
-                # culled primitives are algorithmic work the kernel provably
-                # need not execute; the hardware counter shows what it did run
-                out["roofline"]["executed_flops_per_launch"] = ex
-                out["roofline"]["executed_TFLOPs"] = round(ex / (kavg_ms * 1e-3) / 1e12, 2)
-        else:
-            out["roofline"] = None
+        pmc = (pmc_summary(args.config, args.precision)
+               if world == 1 and args.format == "rgba32f" else {})
+        out["roofline"] = roofline(pmc, flops, kavg_ms, rows * W * lib_bpp(frame))
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline ...")
             out["cpu_baseline"] = cpu_baseline(frame, args.cpu_sample_stride, args.cpu_frames)

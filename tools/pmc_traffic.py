@@ -110,23 +110,25 @@ def main():
     need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
             "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES", "GRBM_GUI_ACTIVE")
     if all(k in res for k in need):
-        # VALU issue model: wave-instructions weighted by their measured issue
-        # cost on one SIMD (tools/valu_rates.hip: add/mul/fma 2.4 cycles,
-        # transcendentals 8.2, min/max/cmp/cndmask 4.2, mov/logic 2.4); the
-        # counters do not split the remainder, so it is bounded both ways.
-        # Kernel cycles per SIMD = GRBM_GUI_ACTIVE / 8 XCDs (GFX-clock cycles).
+        # instruction mix per wave: full-rate add/mul/FMA, transcendentals, and
+        # the remainder (min/max/cmp/cndmask/mov/logic, not split by counters)
         full = res["SQ_INSTS_VALU_ADD_F32"] + res["SQ_INSTS_VALU_MUL_F32"] + res["SQ_INSTS_VALU_FMA_F32"]
         trans = res["SQ_INSTS_VALU_TRANS_F32"]
         other = res["SQ_INSTS_VALU"] - full - trans
-        simds, xcds = 1024, 8
-        kcyc = res["GRBM_GUI_ACTIVE"] / xcds
-        lo = (2.4 * (full + other) + 8.2 * trans) / simds
-        hi = (2.4 * full + 4.2 * other + 8.2 * trans) / simds
-        out["valu_issue_model"] = {
-            "kernel_cycles": kcyc, "issue_cycles_per_simd": [lo, hi],
-            "util": [lo / kcyc, hi / kcyc],
-            "per_wave": {"full_rate": full / res["SQ_WAVES"], "transcendental": trans / res["SQ_WAVES"],
-                         "other": other / res["SQ_WAVES"]}}
+        out["valu_mix_per_wave"] = {"full_rate": full / res["SQ_WAVES"],
+                                    "transcendental": trans / res["SQ_WAVES"],
+                                    "other": other / res["SQ_WAVES"],
+                                    "total": res["SQ_INSTS_VALU"] / res["SQ_WAVES"]}
+    calib = ROOT / "profiles" / "r02_valu_busy_calib.json"
+    if res.get("SQ_ACTIVE_INST_VALU") and res.get("GRBM_GUI_ACTIVE") and calib.exists():
+        # counter-based VALU busy, gfx950 normalisation calibrated on pure
+        # full-rate VALU chains (tools/valu_busy_calib.py): SIMD cycles per
+        # SQ_ACTIVE_INST_VALU unit over 1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs
+        cpu = json.loads(calib.read_text())["cycles_per_unit"]
+        out["valu_busy"] = cpu * res["SQ_ACTIVE_INST_VALU"] / (1024 * res["GRBM_GUI_ACTIVE"] / 8)
+        out["valu_busy_method"] = (f"{cpu} cycles/unit x SQ_ACTIVE_INST_VALU / (1024 SIMDs x "
+                                   "GRBM_GUI_ACTIVE / 8); a lower bound (half-rate "
+                                   "min/max/cmp count one unit)")
     if res.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in res:
         out["valu_lane_util"] = res["SQ_THREAD_CYCLES_VALU"] / (64 * res["SQ_ACTIVE_INST_VALU"])
     p = outdir / f"pmc_{args.config}_{args.precision}.json"   # copy into profiles/ to commit
