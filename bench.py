@@ -93,6 +93,11 @@ def parse():
                          "a single-device render bit for bit")
     ap.add_argument("--no-display", action="store_true",
                     help="skip the extra RGBA8-framebuffer measurement reported beside value")
+    ap.add_argument("--comm-lib", default=None,
+                    help="library with the RCCL symbols the native driver loads (default: the "
+                         "librccl this process has mapped); with --backend gloo, a stand-in "
+                         "such as tests/shmcomm/libshmcomm.so runs the native driver with "
+                         "several ranks on one GPU")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -270,7 +275,8 @@ def main():
             try:
                 drv = NativeFrameDriver(f32, rank, world, dev, shares=shares, nbuf=nbuf,
                                         lag=lag if world > 1 else 1,
-                                        dist=dist if world > 1 else None)
+                                        dist=dist if world > 1 else None,
+                                        rccl_path=args.comm_lib)
             except Exception as e:  # noqa: BLE001 - reported, then the fallback
                 log(f"[bench] rank {rank}: native driver unavailable ({e})")
                 ok = False
@@ -306,8 +312,8 @@ def main():
         """warmup + `steps` timed frames of `fr` through a frame driver; returns
         (max-over-ranks seconds, per-launch kernel ms list, driver)."""
         # (gloo rehearsals share one GPU between ranks, which RCCL refuses)
-        use_native = args.driver == "native" and nbuf >= 2 and (world == 1 or
-                                                                  args.backend == "nccl")
+        use_native = args.driver == "native" and nbuf >= 2 and (
+            world == 1 or args.backend == "nccl" or args.comm_lib is not None)
         drv = native_driver(fr) if use_native else None
         if drv is not None:
             warm_clocks()

@@ -16,8 +16,18 @@
 // SDF3D_RUN_ID (default: torchrun's TORCHELASTIC_RUN_ID); SDF3D_RCCL names
 // the librccl to load (default librccl.so.1); SDF3D_ROOT_AS_PEER=1 makes
 // rank 0 ship its rows to itself (the multi-rank sequence on one GPU).
+//
+// Navigation: by default frame i orbits the camera by 360 i / frames degrees;
+// SDF3D_NAV=arcball drives V_mat from sdf::Arcball (the reference's mouse and
+// gamepad navigation, main.cpp:37-45, :93-94) fed with a scripted input
+// sequence (nav_input: orbit drag, pan drag, release, gamepad sticks), and
+//   sdf_main --views N
+// prints the first N V_mats of that sequence (no GPU work; the tests compare
+// them with sdf3d_amd.camera.Arcball fed the same script).
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <string>
 
@@ -29,6 +39,33 @@ std::string env(const char* name, const char* dflt) {
   const char* v = std::getenv(name);
   return v && *v ? v : dflt;
 }
+
+// The scripted navigation input of frame i (period 90 frames at 60 Hz),
+// restated in tests/test_camera.py nav_input.
+void nav_input(sdf::Arcball& a, int i) {
+  const double dt = 1.0 / 60.0;
+  const int ph = i % 90;
+  if (ph < 30) a.mouse(dt, 0.004, 0.0015, true, false);          // orbit drag
+  else if (ph < 45) a.mouse(dt, -0.002, 0.001, false, true);     // pan drag
+  else if (ph < 60) a.mouse(dt, 0.0, 0.0, false, false);         // released: decay
+  else if (ph < 80) a.gamepad(dt, 0.8, -0.5, 0.2, 0.35);        // sticks (rx inside the deadzone)
+  else a.gamepad(dt, 0.1, 0.0, 0.0, 0.0);                        // sticks released
+}
+
+// V_mat of frame i under SDF3D_NAV (see the header comment).
+struct Navigator {
+  bool arcball = env("SDF3D_NAV", "orbit") == "arcball";
+  sdf::Arcball ball;
+  int next = 0;
+  void frame(sdf::Frame& f, int i, int frames) {
+    if (!arcball) {
+      f.orbit(360.0f * i / frames, 0.0f);
+      return;
+    }
+    while (next <= i) nav_input(ball, next++);
+    ball.apply(f);
+  }
+};
 
 int run_driver(sdf::Frame f, int frames, const std::string& out) {
   const int rank = std::atoi(env("RANK", "0").c_str());
@@ -66,9 +103,10 @@ int run_driver(sdf::Frame f, int frames, const std::string& out) {
   int64_t last = -1;
   for (int i = 0; i < 5; ++i) last = drv.step();  // warm-up
   drv.drain();
+  Navigator nav;
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < frames; ++i) {
-    f.orbit(360.0f * i / frames, 0.0f);             // the arcball's V_mat (main.cpp:93-94)
+    nav.frame(f, i, frames);                        // the arcball's V_mat (main.cpp:93-94)
     drv.set_camera(f.camera);
     last = drv.step();
   }
@@ -89,6 +127,20 @@ int run_driver(sdf::Frame f, int frames, const std::string& out) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[1]) == "--views") {
+    sdf::Arcball ball;
+    float v[16];
+    for (int i = 0; i < std::atoi(argv[2]); ++i) {
+      nav_input(ball, i);
+      ball.view(v);
+      for (int k = 0; k < 16; ++k) {
+        uint32_t u;
+        std::memcpy(&u, &v[k], 4);
+        std::printf("%08x%c", u, k == 15 ? '\n' : ' ');
+      }
+    }
+    return 0;
+  }
   const int W = argc > 1 ? std::atoi(argv[1]) : 800;   // main.cpp:4 SX
   const int H = argc > 2 ? std::atoi(argv[2]) : 600;   // main.cpp:5 SY
   const int frames = argc > 3 ? std::atoi(argv[3]) : 8;
@@ -129,8 +181,9 @@ int main(int argc, char** argv) {
     sdf::check_hip(hipEventCreate(&t1), "hipEventCreate");
     {
       sdf::Renderer r(W, H, stream);
+      Navigator nav;
       for (int i = 0; i < frames; ++i) {
-        f.orbit(360.0f * i / frames, 0.0f);
+        nav.frame(f, i, frames);
         sdf::check_hip(hipEventRecord(t0, stream), "hipEventRecord");
         r.render(f);
         sdf::check_hip(hipEventRecord(t1, stream), "hipEventRecord");

@@ -14,10 +14,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <cstdio>
 #include <stdexcept>
@@ -40,6 +43,15 @@ inline void check(int rc, const char* what) {
 }
 inline void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+// The loaded libsdf3d must implement the ABI these headers describe (struct
+// layouts and signatures change with SDF_ABI_VERSION); checked once by every
+// object that calls into it.
+inline void check_abi() {
+  static const int v = sdf_abi_version();
+  if (v != SDF_ABI_VERSION)
+    throw Error(SDF_E_UNSUPPORTED, "libsdf3d ABI " + std::to_string(v) + " != headers' " +
+                                       std::to_string(SDF_ABI_VERSION));
 }
 
 // Scene builder: primitives combined left to right into d (d starts at +INF,
@@ -111,6 +123,7 @@ struct Frame {
   // The reference shader's hard-coded frame (voxel_fragment.frag:15-23,
   // :54-81, :178-189, :205) at width x height (<= 0: 800 x 600, main.cpp:4-5).
   static Frame reference(int width = 0, int height = 0) {
+    check_abi();
     Frame f;
     check(sdf_defaults(&f.scene, &f.camera, &f.light, &f.material, &f.params, width, height),
           "sdf_defaults");
@@ -130,12 +143,89 @@ struct Frame {
   }
 };
 
+// Arcball navigation producing V_mat: the reference
+// drives V_mat from Neutrino's mouse and gamepad navigation with these rates
+// (main.cpp:37-45: orbit 1 rev/s, pan 5 m/s, decay 1.25 s; gamepad orbit 1,
+// pan 1, decay 1.25, deadzone 0.30), called once per frame (:93-94).
+// Neutrino's implementation is not vendored, so the dynamics are this
+// framework's own (parity unpinned), identical to sdf3d_amd/camera.py (the
+// tests compare the two sequences bit for bit):
+//   * while a mouse button drags, orbit (or pan) velocity = rate * motion / dt;
+//     released, the velocity decays by exp(-dt / decay_time) per update;
+//   * a gamepad stick outside the deadzone sets the velocity to
+//     rate * 2 pi (orbit, rev/s) or rate (pan) times the stick value rescaled
+//     from [deadzone, 1] to [0, 1]; inside it, the velocity decays;
+//   * pitch is clamped to [-pi/2, pi/2]; V_mat = T(pan) * Rx(pitch) * Ry(yaw).
+// All arithmetic in double, the matrix rounded to float once.
+class Arcball {
+ public:
+  struct Rates {
+    double orbit_rate = 1.0, pan_rate = 5.0, decay_time = 1.25;     // mouse, main.cpp:37-39
+    double pad_orbit_rate = 1.0, pad_pan_rate = 1.0, pad_decay_time = 1.25,
+           pad_deadzone = 0.30;                                       // gamepad, main.cpp:42-45
+  };
+  Arcball() = default;
+  explicit Arcball(const Rates& r) : r_(r) {}
+
+  // Mouse: pointer motion (dx, dy) in normalised screen units over dt seconds.
+  void mouse(double dt, double dx, double dy, bool orbit, bool pan) {
+    if (!(dt > 0)) return;
+    if (orbit) vyaw_ = r_.orbit_rate * dx / dt, vpitch_ = r_.orbit_rate * dy / dt;
+    if (pan) vpx_ = r_.pan_rate * dx / dt, vpy_ = r_.pan_rate * dy / dt;
+    integrate(dt, !orbit, !pan, r_.decay_time);
+  }
+  // Gamepad: left stick (lx, ly) orbits, right stick (rx, ry) pans, in [-1, 1].
+  void gamepad(double dt, double lx, double ly, double rx, double ry) {
+    if (!(dt > 0)) return;
+    const double ax = dead(lx), ay = dead(ly), bx = dead(rx), by = dead(ry);
+    const bool orbit = ax != 0.0 || ay != 0.0, pan = bx != 0.0 || by != 0.0;
+    const double two_pi = 2.0 * M_PI;
+    if (orbit) vyaw_ = r_.pad_orbit_rate * two_pi * ax, vpitch_ = r_.pad_orbit_rate * two_pi * ay;
+    if (pan) vpx_ = r_.pad_pan_rate * bx, vpy_ = r_.pad_pan_rate * by;
+    integrate(dt, !orbit, !pan, r_.pad_decay_time);
+  }
+  // V_mat, column-major float (sdf_camera.view).
+  void view(float* out16) const {
+    const double cy = std::cos(yaw_), sy = std::sin(yaw_), cp = std::cos(pitch_),
+                 sp = std::sin(pitch_);
+    const double m[4][4] = {{cy, 0, sy, pan_x_}, {sp * sy, cp, -sp * cy, pan_y_},
+                            {-cp * sy, sp, cp * cy, 0}, {0, 0, 0, 1}};
+    for (int c = 0; c < 4; ++c)
+      for (int r = 0; r < 4; ++r) out16[c * 4 + r] = static_cast<float>(m[r][c]);
+  }
+  void apply(Frame& f) const { view(f.camera.view); }
+  double yaw() const { return yaw_; }
+  double pitch() const { return pitch_; }
+
+ private:
+  double dead(double a) const {
+    const double z = r_.pad_deadzone, m = std::fabs(a);
+    if (!(m > z)) return 0.0;
+    return std::copysign(std::min((m - z) / (1.0 - z), 1.0), a);
+  }
+  void integrate(double dt, bool decay_orbit, bool decay_pan, double tau) {
+    yaw_ += vyaw_ * dt;
+    pitch_ = std::max(-M_PI / 2, std::min(M_PI / 2, pitch_ + vpitch_ * dt));
+    pan_x_ += vpx_ * dt;
+    pan_y_ += vpy_ * dt;
+    if (decay_orbit || decay_pan) {
+      const double k = tau > 0 ? std::exp(-dt / tau) : 0.0;
+      if (decay_orbit) vyaw_ *= k, vpitch_ *= k;
+      if (decay_pan) vpx_ *= k, vpy_ *= k;
+    }
+  }
+  Rates r_;
+  double yaw_ = 0, pitch_ = 0, pan_x_ = 0, pan_y_ = 0;
+  double vyaw_ = 0, vpitch_ = 0, vpx_ = 0, vpy_ = 0;
+};
+
 // Owns a device framebuffer and renders frames into it on one HIP stream.
 // The buffer holds width x height pixels of up to 16 bytes (any sdf_format).
 class Renderer {
  public:
   Renderer(int width, int height, hipStream_t stream = nullptr)
       : w_(width), h_(height), stream_(stream) {
+    check_abi();
     check_hip(hipMalloc(&rgba_, size_t(w_) * h_ * 16), "hipMalloc");
   }
   ~Renderer() { if (rgba_) (void)hipFree(rgba_); }
@@ -187,14 +277,19 @@ class Comm {
  public:
   using Id = std::vector<unsigned char>;
   static Id unique_id(const std::string& rccl_path = "") {
+    check_abi();
     Id id(SDF_COMM_ID_BYTES);
     check(sdf_comm_unique_id(rccl_path.empty() ? nullptr : rccl_path.c_str(), id.data()),
           "sdf_comm_unique_id");
     return id;
   }
-  Comm(const Id& id, int world, int rank, const std::string& rccl_path = "") {
+  // Blocks until every rank has joined, at most timeout_ms (then throws
+  // SDF_E_TIMEOUT: a peer that failed, or an id that is not this launch's).
+  Comm(const Id& id, int world, int rank, const std::string& rccl_path = "",
+       int timeout_ms = 120000) {
+    check_abi();
     check(sdf_comm_create(rccl_path.empty() ? nullptr : rccl_path.c_str(), id.data(), world, rank,
-                          &c_),
+                          timeout_ms, &c_),
           "sdf_comm_create");
   }
   ~Comm() { if (c_) (void)sdf_comm_destroy(c_); }
@@ -210,28 +305,65 @@ class Comm {
 // local disk or /dev/shm): rank 0 writes `name` atomically (write, then
 // rename), the others wait for it.  Pure-C++ launches (no MPI, no Python)
 // use this; a Python host uses torch.distributed (sdf3d_amd/driver.py).
+//
+// A file left by an earlier launch that died before rank 0 removed it must
+// not be taken for this launch's.  So the file carries a launch tag (the
+// launcher's MASTER_ADDR/MASTER_PORT, TORCHELASTIC_RUN_ID and
+// TORCHELASTIC_RESTART_COUNT, plus SDF3D_LAUNCH_NONCE when the launcher
+// sets one) that peers compare with their own, and peers ignore a file
+// written before their own first call here, less `skew_s` (ranks of one
+// launch start within seconds of each other).  An id that still slips
+// through cannot hang anyone: Comm's join gives up after its timeout.
+inline std::string launch_tag() {
+  std::string t;
+  for (const char* k : {"MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+                        "TORCHELASTIC_RESTART_COUNT", "SDF3D_LAUNCH_NONCE"}) {
+    const char* v = std::getenv(k);
+    t += std::string(k) + "=" + (v ? v : "") + ";";
+  }
+  return t;
+}
+
 inline Comm::Id exchange_id(const std::string& dir, const std::string& name, int rank,
-                            const std::string& rccl_path = "", double timeout_s = 120.0) {
+                            const std::string& rccl_path = "", double timeout_s = 120.0,
+                            double skew_s = 30.0) {
+  static const auto first_call = std::chrono::system_clock::now();
   const std::string path = dir + "/" + name;
+  const std::string tag = launch_tag();
   if (rank == 0) {
     Comm::Id id = Comm::unique_id(rccl_path);
     const std::string tmp = path + ".tmp";
+    const uint32_t n = static_cast<uint32_t>(tag.size());
     FILE* fp = std::fopen(tmp.c_str(), "wb");
-    if (!fp || std::fwrite(id.data(), 1, id.size(), fp) != id.size() || std::fclose(fp) != 0 ||
+    if (!fp || std::fwrite(&n, sizeof(n), 1, fp) != 1 ||
+        std::fwrite(tag.data(), 1, n, fp) != n ||
+        std::fwrite(id.data(), 1, id.size(), fp) != id.size() || std::fclose(fp) != 0 ||
         std::rename(tmp.c_str(), path.c_str()) != 0)
       throw std::runtime_error("cannot write " + path);
     return id;
   }
+  const auto not_before = first_call - std::chrono::milliseconds(long(skew_s * 1e3));
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    if (FILE* fp = std::fopen(path.c_str(), "rb")) {
-      Comm::Id id(SDF_COMM_ID_BYTES);
-      const size_t n = std::fread(id.data(), 1, id.size(), fp);
-      std::fclose(fp);
-      if (n == id.size()) return id;
+    struct stat sb;
+    if (stat(path.c_str(), &sb) == 0 &&
+        std::chrono::system_clock::from_time_t(sb.st_mtime) >= not_before) {
+      if (FILE* fp = std::fopen(path.c_str(), "rb")) {
+        uint32_t n = 0;
+        std::string got;
+        Comm::Id id(SDF_COMM_ID_BYTES);
+        bool ok = std::fread(&n, sizeof(n), 1, fp) == 1 && n < (1u << 16);
+        if (ok) {
+          got.resize(n);
+          ok = std::fread(&got[0], 1, n, fp) == n &&
+               std::fread(id.data(), 1, id.size(), fp) == id.size();
+        }
+        std::fclose(fp);
+        if (ok && got == tag) return id;
+      }
     }
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
-      throw std::runtime_error("timed out waiting for " + path);
+      throw std::runtime_error("timed out waiting for " + path + " of this launch");
     std::this_thread::sleep_for(std::chrono::milliseconds(5));
   }
 }
@@ -245,6 +377,7 @@ class FrameDriver {
   FrameDriver(const Frame& f, const sdf_driver_config& cfg, Comm* lengths = nullptr,
               Comm* data = nullptr)
       : w_(f.params.width), h_(f.params.height), format_(f.params.output_format) {
+    check_abi();
     check(sdf_driver_create(&f.scene, &f.camera, &f.light, &f.material, &f.params, &cfg,
                             lengths ? lengths->get() : nullptr, data ? data->get() : nullptr, &d_),
           "sdf_driver_create");

@@ -56,7 +56,7 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 6   /* 6: sdf_tiling.run_step (interleaved runs) */
+#define SDF_ABI_VERSION 7   /* 7: sdf_comm_create timeout; 6: sdf_tiling.run_step */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -405,10 +405,11 @@ typedef struct sdf_comm sdf_comm;
 typedef struct sdf_driver sdf_driver;
 
 int sdf_comm_unique_id(const char* rccl_path, void* id /* SDF_COMM_ID_BYTES */);
-/* Collective over nranks processes (blocks until all have joined); the
- * current HIP device is the communicator's. */
+/* Collective over nranks processes (blocks until all have joined, at most
+ * timeout_ms, <= 0: 120000; then SDF_E_TIMEOUT); the current HIP device is
+ * the communicator's. */
 int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
-                    sdf_comm** comm);
+                    int32_t timeout_ms, sdf_comm** comm);
 int sdf_comm_destroy(sdf_comm* comm);
 
 /* SDF_DRIVER_ROOT_AS_PEER: rank 0 ships its rows as a TILES stream to itself
@@ -439,8 +440,9 @@ int sdf_driver_step(sdf_driver* driver, int64_t* frame_index);
 /* Ship every rendered frame and wait until all work of this rank is done. */
 int sdf_driver_drain(sdf_driver* driver);
 /* Rank 0 (or world 1): device pointer of frame `index`'s framebuffer
- * (height * width pixels), one of the last nbuf frames, assembled once it
- * has been shipped (after sdf_driver_drain for the last `lag`). */
+ * (height * width pixels), one of the last nbuf frames.  With collectives
+ * the frame must have been shipped (the last `lag` frames stepped are, after
+ * sdf_driver_drain): an index not shipped yet is SDF_E_INVALID_ARG. */
 int sdf_driver_frame(sdf_driver* driver, int64_t index, void** rgba);
 /* Copy frame `index` (as sdf_driver_frame) into the caller's device buffer
  * `dst` of `bytes` (>= the frame's size), asynchronously on `stream` after

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 6
+SDF_ABI_VERSION = 7
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -129,7 +129,7 @@ SIGNATURES = {
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                               C.c_void_p, C.c_void_p]),
     "sdf_comm_unique_id": (C.c_int, [C.c_char_p, C.c_void_p]),
-    "sdf_comm_create": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32,
+    "sdf_comm_create": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                   _P(C.c_void_p)]),
     "sdf_comm_destroy": (C.c_int, [C.c_void_p]),
     "sdf_driver_create": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light),

@@ -38,10 +38,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sdf_abi.h"
@@ -140,6 +143,7 @@ struct sdf_driver {
   std::vector<hipEvent_t> ev_render, ev_size, ev_gather;
   std::deque<long long> pending;
   long long next = 0;
+  long long shipped = -1;  // highest frame whose streams are shipped and decoded (rank 0)
   int error = SDF_OK;  // sticky: a failed driver refuses further frames
   // host-time accounting (sdf_driver_stats): seconds inside step/drain, and
   // the part of it spent waiting for the GPU or a peer
@@ -247,6 +251,7 @@ int ship(sdf_driver* d, long long j) {
                                                      d->rs[b]));
     d->t_decode += seconds_since(tg);
   }
+  if (rc == SDF_OK) d->shipped = j;
   return fail(d, rc);
 }
 
@@ -282,19 +287,51 @@ int sdf_comm_unique_id(const char* rccl_path, void* id) {
   return SDF_OK;
 }
 
+// ncclCommInitRank blocks until every rank has joined.  It runs on a helper
+// thread so that the caller gets SDF_E_TIMEOUT after `timeout_ms` when a
+// peer never joins (a peer that failed, or an id from an earlier run): the
+// helper is then left blocked, and the process is expected to report the
+// error and exit.
 int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
-                    sdf_comm** comm) {
+                    int32_t timeout_ms, sdf_comm** comm) {
   if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return SDF_E_INVALID_ARG;
   *comm = nullptr;
   Rccl* R = load_rccl(rccl_path);
   if (!R) return SDF_E_COMM;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return SDF_E_NO_DEVICE;
+  struct Init {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclResult_t rc = ncclSuccess;
+    ncclComm_t c = nullptr;
+  };
+  auto st = std::make_shared<Init>();
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
-  ncclComm_t c = nullptr;
-  if (R->CommInitRank(&c, nranks, uid, rank) != ncclSuccess) return SDF_E_COMM;
-  *comm = new sdf_comm{R, c, nranks, rank, dev};
+  std::thread([st, R, uid, nranks, rank, dev] {
+    (void)hipSetDevice(dev);
+    ncclComm_t c = nullptr;
+    const ncclResult_t rc = R->CommInitRank(&c, nranks, uid, rank);
+    std::lock_guard<std::mutex> lock(st->mu);
+    if (st->abandoned) {  // the caller gave up: nobody will use it
+      if (rc == ncclSuccess && c) R->CommAbort(c);
+      return;
+    }
+    st->rc = rc;
+    st->c = c;
+    st->done = true;
+    st->cv.notify_all();
+  }).detach();
+  std::unique_lock<std::mutex> lock(st->mu);
+  const auto limit = std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 120000);
+  if (!st->cv.wait_for(lock, limit, [&] { return st->done; })) {
+    st->abandoned = true;
+    return SDF_E_TIMEOUT;
+  }
+  if (st->rc != ncclSuccess || !st->c) return SDF_E_COMM;
+  *comm = new sdf_comm{R, st->c, nranks, rank, dev};
   return SDF_OK;
 }
 
@@ -553,6 +590,9 @@ int sdf_driver_frame(sdf_driver* d, int64_t index, void** rgba) {
   *rgba = nullptr;
   if (!d->root || index < 0 || index >= d->next || index < d->next - d->nbuf)
     return SDF_E_INVALID_ARG;
+  // with collectives a frame holds the peers' rows only once it has been
+  // shipped (the last `lag` frames stepped: after sdf_driver_drain)
+  if (d->collectives && index > d->shipped) return SDF_E_INVALID_ARG;
   *rgba = d->frames[index % d->nbuf];
   return SDF_OK;
 }

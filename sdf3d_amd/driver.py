@@ -45,26 +45,51 @@ def loaded_rccl_path() -> str:
 
 class Comm:
     """One RCCL communicator over the torch.distributed world (collective:
-    every rank constructs it, in the same order)."""
+    every rank constructs it, in the same order).
 
-    def __init__(self, dist, device, rccl_path: str | None = None):
+    Failure is agreed, never one-sided: rank 0 broadcasts a status byte with
+    the id (so a failed sdf_comm_unique_id fails every rank at the same
+    collective), sdf_comm_create gives up after `timeout_ms` when a peer never
+    joins, and the ranks all-reduce their outcome, so either every rank holds
+    the communicator or every rank raises (and bench.py falls back on all of
+    them together)."""
+
+    def __init__(self, dist, device, rccl_path: str | None = None, timeout_ms: int = 120000):
         import torch
         self.lib = abi.load_library()
         self.path = (rccl_path or loaded_rccl_path()).encode()
+        self.handle = C.c_void_p()
         rank, world = dist.get_rank(), dist.get_world_size()
-        uid = torch.zeros(abi.COMM_ID_BYTES, dtype=torch.uint8)
+        msg = torch.zeros(abi.COMM_ID_BYTES + 1, dtype=torch.uint8)   # [ok, id]
+        err = None
         if rank == 0:
             buf = (C.c_uint8 * abi.COMM_ID_BYTES)()
-            abi.check(self.lib.sdf_comm_unique_id(self.path, buf), "sdf_comm_unique_id")
-            uid = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8)
+            rc = self.lib.sdf_comm_unique_id(self.path, buf)
+            if rc == abi.SDF_OK:
+                msg[0] = 1
+                msg[1:] = torch.frombuffer(bytearray(bytes(buf)), dtype=torch.uint8)
+            else:
+                err = abi.SdfError(rc, "sdf_comm_unique_id")
         on_dev = dist.get_backend() == "nccl"
-        t = uid.to(device) if on_dev else uid
+        t = msg.to(device) if on_dev else msg
         dist.broadcast(t, src=0)
-        raw = bytes(t.cpu().numpy().tobytes())
-        self.handle = C.c_void_p()
-        with torch.cuda.device(device):
-            abi.check(self.lib.sdf_comm_create(self.path, raw, world, rank,
-                                               C.byref(self.handle)), "sdf_comm_create")
+        msg = t.cpu()
+        ok = int(msg[0]) == 1
+        if ok:
+            raw = bytes(msg[1:].numpy().tobytes())
+            with torch.cuda.device(device):
+                rc = self.lib.sdf_comm_create(self.path, raw, world, rank, int(timeout_ms),
+                                              C.byref(self.handle))
+            if rc != abi.SDF_OK:
+                ok, err = False, abi.SdfError(rc, "sdf_comm_create")
+        elif err is None:
+            err = abi.SdfError(abi.SDF_E_COMM, "rank 0 could not make a communicator id")
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        flag = flag.to(device) if on_dev else flag
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) != 1:
+            self.close()
+            raise err or abi.SdfError(abi.SDF_E_COMM, "a peer could not join the communicator")
 
     def close(self):
         if self.handle:
@@ -78,7 +103,8 @@ class NativeFrameDriver:
     rank 0's frame i (one of the last ``nbuf``) into a torch tensor."""
 
     def __init__(self, frame: Frame, rank: int, world: int, device, shares=(1, 1), nbuf: int = 4,
-                 lag: int = 2, dist=None, root_as_peer: bool = False, timeout_ms: int = 60000):
+                 lag: int = 2, dist=None, root_as_peer: bool = False, timeout_ms: int = 60000,
+                 rccl_path: str | None = None):
         import torch
         self.torch = torch
         self.lib = abi.load_library()
@@ -93,7 +119,12 @@ class NativeFrameDriver:
         if world > 1 or root_as_peer:
             if dist is None:
                 raise ValueError("a multi-rank driver needs torch.distributed for its comm ids")
-            self.comms = [Comm(dist, self.device), Comm(dist, self.device)]
+            try:
+                for _ in range(2):
+                    self.comms.append(Comm(dist, self.device, rccl_path))
+            except Exception:
+                self._close_comms()
+                raise
         self.handle = C.c_void_p()
         with torch.cuda.device(self.device):
             rc = self.lib.sdf_driver_create(

@@ -104,3 +104,114 @@ def test_native_bad_config():
     ft.params.output_format = abi.FORMAT_TILES
     with pytest.raises(abi.SdfError):
         NativeFrameDriver(ft, 0, 1, "cuda:0", nbuf=3, lag=1)      # TILES is a wire, not a frame
+
+
+ROOT = __import__("pathlib").Path(__file__).resolve().parent.parent
+SHMCOMM = ROOT / "tests" / "shmcomm" / "libshmcomm.so"
+
+
+def test_frame_not_shipped_is_refused(nccl_world1):
+    """a frame whose peers' rows have not been shipped yet (the
+    last `lag` frames stepped, before sdf_driver_drain) is refused, not
+    handed out half-assembled."""
+    from sdf3d_amd import abi, scenes
+    from sdf3d_amd.driver import NativeFrameDriver
+    f = scenes.config("C3", 96, 64, precision=abi.PRECISION_FAST)
+    drv = NativeFrameDriver(f, 0, 1, "cuda:0", nbuf=4, lag=2, dist=nccl_world1,
+                            root_as_peer=True)
+    idx = [drv.step() for _ in range(3)]
+    with pytest.raises(abi.SdfError):
+        drv.read_frame(idx[-1])          # not shipped yet (lag 2)
+    drv.read_frame(idx[0])               # shipped at step 2
+    drv.drain()
+    got = drv.read_frame(idx[-1])
+    torch.cuda.synchronize()
+    drv.close()
+    assert torch.equal(got.view(torch.int32), _reference(f).view(torch.int32))
+
+
+@pytest.mark.parametrize("nproc,cfg,shares", [(2, "C3", None), (3, "C3", "1:2"), (8, "C3", None),
+                                              (8, "C4", None)])
+def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
+    """The native C++ driver's multi-rank sequence (render, RCCL-style length
+    all-gather, send/recv of the TILES streams to rank 0, decode) with
+    `nproc` ranks sharing this GPU: bench.py --driver native over the
+    stand-in communications library tests/shmcomm (RCCL refuses two ranks on
+    one GPU).  Rank 0's assembled last frame must equal a single-device
+    render bit for bit; the 8-rank C4 case is the round-end N = 8 bench's
+    configuration (4K, default 1:3 shares)."""
+    import json
+    import subprocess
+    import sys
+    assert SHMCOMM.exists(), "build() must produce tests/shmcomm/libshmcomm.so"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "6", "--warmup", "2",
+           "--backend", "gloo", "--comm-lib", str(SHMCOMM), "--driver", "native",
+           "--config", cfg, "--no-display", "--clock-warm-s", "0"]
+    if shares:
+        cmd += ["--shares", shares]
+    env = dict(os.environ, SHMCOMM_TIMEOUT_MS="60000")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == nproc and d["frame_verified"] is True, d
+    assert d["config"]["driver"].startswith("native"), d["config"]
+    assert d["config"]["wire"] == "tiles"
+    if nproc == 8:
+        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 1 / others 3")
+
+
+def _read_ppm(path):
+    import numpy as np
+    data = open(path, "rb").read()
+    parts = data.split(b"\n", 3)
+    w, h = map(int, parts[1].split())
+    return np.frombuffer(parts[3], dtype=np.uint8).reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cpp_driver_multirank_arcball(tmp_path, world):
+    """examples/sdf_main.cpp as `world` processes on this GPU (RANK /
+    WORLD_SIZE set, ids exchanged through files, stand-in communications
+    library), camera from sdf::Arcball's scripted navigation (SDF3D_NAV):
+    rank 0's last frame equals the Python path's render of the same V_mat
+    (sdf3d_amd.camera.Arcball) to 1 LSB of the 8-bit image, and that render
+    passes the oracle parity policy."""
+    import subprocess
+    import sys
+
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle
+    from parity import assert_parity, quantize, report
+    from sdf3d_amd import Renderer, abi, scenes
+    from test_camera import nav_views
+    exe = ROOT / "sdf3d_amd" / "bin" / "sdf_main"
+    frames, W, H = 40, 160, 96
+    out = tmp_path / "f.ppm"
+    procs = []
+    port = str(_free_port())     # the launch tag of the id files (sdf3d.hpp exchange_id)
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                   SDF3D_RCCL=str(SHMCOMM), SDF3D_ID_DIR=str(tmp_path),
+                   SDF3D_RUN_ID=f"t{os.getpid()}_{world}", SDF3D_NAV="arcball",
+                   SHMCOMM_TIMEOUT_MS="60000", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([str(exe), str(W), str(H), str(frames), str(out), "csg8"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (so, se) in zip(procs, outs):
+        assert p.returncode == 0, se[-2000:]
+    assert f"rank 0 of {world}" in outs[0][0]
+    img = _read_ppm(out)
+    f = scenes.config("C3", W, H, precision=abi.PRECISION_FAST)
+    scenes.set_view(f, nav_views(frames)[-1])
+    rd = Renderer("cuda:0")
+    rgba, st = rd.render(f, steps=True)
+    torch.cuda.synchronize()
+    rgba, st = rgba.cpu().numpy(), st.cpu().numpy()
+    want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
+    assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
+    ref, rst = oracle.render(f)
+    assert_parity(report(rgba, st, ref, rst, oracle.render(f, twin=True)[0]), what="arcball")

@@ -202,3 +202,43 @@ def test_share_rows_balanced_on_4k(world, shares, busiest):
     assert sum(rows) == 2160 and max(rows[1:]) == busiest
     ids = np.concatenate([owned_row_ids(2160, r, world, 8, shares) for r in range(world)])
     assert np.array_equal(np.sort(ids), np.arange(2160))
+
+
+def _comm_fail_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sdf3d_amd import abi
+        from sdf3d_amd.driver import Comm
+        try:
+            # rank 0 cannot load the communications library: it must not be
+            # the only rank to give up (the others would wait in a collective)
+            Comm(dist, "cpu", rccl_path="/nonexistent/librccl.so" if rank == 0 else None)
+            q.put((rank, "created"))
+        except abi.SdfError as e:
+            q.put((rank, f"raised {e.code}"))
+        # the ranks are still in step: a later collective completes
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        q.put((rank, f"sum {int(t.item())}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_failure_is_agreed():
+    """sdf3d_amd.driver.Comm fails on every rank together (status
+    broadcast with the id), so no rank is left blocked in a collective."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_comm_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    got = sorted(q.get(timeout=10) for _ in range(2 * world))
+    from sdf3d_amd import abi
+    for r in range(world):
+        assert (r, f"raised {abi.SDF_E_COMM}") in got and (r, f"sum {world}") in got
