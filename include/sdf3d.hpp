@@ -416,6 +416,19 @@ class FrameDriver {
   sdf_driver* d_ = nullptr;
 };
 
+// One RGBA32F frame across several devices of this process (sdf_render_multi):
+// devices[0] holds `rgba` and `stream`; the others render TILES streams the
+// root decodes through peer-mapped memory.  Successive calls on one stream.
+inline void render_multi(const Frame& f, const std::vector<int>& devices, float* rgba,
+                         hipStream_t stream, int share_root = 0, int share_peer = 0) {
+  check_abi();
+  std::vector<int32_t> d(devices.begin(), devices.end());
+  check(sdf_render_multi(&f.scene, &f.camera, &f.light, &f.material, &f.params,
+                         static_cast<int32_t>(d.size()), d.data(), share_root, share_peer, rgba,
+                         stream),
+        "sdf_render_multi");
+}
+
 // Binary PPM of an RGBA float framebuffer, clamped and quantised to 8 bits
 // (what the reference's window would show), flipped to top-down row order.
 inline void write_ppm(const std::string& path, const std::vector<float>& rgba, int w, int h) {

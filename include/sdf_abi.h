@@ -56,7 +56,7 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 7   /* 7: sdf_comm_create timeout; 6: sdf_tiling.run_step */
+#define SDF_ABI_VERSION 7   /* 7: sdf_comm_create timeout, sdf_render_multi */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -456,6 +456,28 @@ int sdf_driver_read_frame(sdf_driver* driver, int64_t index, void* dst, int64_t 
  * their copies and events), out[5] RCCL send/recv groups, out[6] decodes. */
 int sdf_driver_stats(sdf_driver* driver, double* out, int32_t n);
 int sdf_driver_destroy(sdf_driver* driver);
+
+/* ---- single-process multi-device frames -------------------------------------
+ * One frame rendered across `ndev` devices of THIS process (the reference's
+ * host is one process, main.cpp:34-110): devices[0] is the root and holds
+ * `rgba` (width * height RGBA32F pixels, params->output_format must be
+ * SDF_FORMAT_RGBA32F); `stream` is a stream of the root device.  Rows are
+ * shared as by the driver (sdf_share_tiling with share_root : share_peer
+ * blocks, <= 0: the measured defaults): the root renders its rows into
+ * `rgba`, every other device its rows as a TILES stream into a buffer of its
+ * own, and the root decodes those streams in place through peer-mapped
+ * memory (hipDeviceEnablePeerAccess).  Asynchronous: the frame is complete
+ * for work enqueued on `stream` after the call.  Successive calls must be
+ * ordered (the same `stream`): they share the library's buffers for this
+ * device list, two sets alternating so the peers render the next frame while
+ * the root decodes this one.  A device may be listed more than once (its
+ * shares then render on it in turn).  The current device is left unchanged. */
+int sdf_render_multi(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                     const sdf_material* material, const sdf_params* params, int32_t ndev,
+                     const int32_t* devices, int32_t share_root, int32_t share_peer, void* rgba,
+                     void* stream);
+/* Wait for and free the buffers sdf_render_multi keeps. */
+int sdf_render_multi_release(void);
 
 /* Short description of a status code. */
 const char* sdf_strerror(int code);

@@ -128,6 +128,10 @@ SIGNATURES = {
                                            C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                               C.c_void_p, C.c_void_p]),
+    "sdf_render_multi": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light),
+                                   _P(sdf_material), _P(sdf_params), C.c_int32, C.c_void_p,
+                                   C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "sdf_render_multi_release": (C.c_int, []),
     "sdf_comm_unique_id": (C.c_int, [C.c_char_p, C.c_void_p]),
     "sdf_comm_create": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                   _P(C.c_void_p)]),

@@ -84,6 +84,9 @@ struct DecodeParts {
   int rows[SDF_MAX_DECODE_PARTS], first_block[SDF_MAX_DECODE_PARTS],
       block_stride[SDF_MAX_DECODE_PARTS], block_rows[SDF_MAX_DECODE_PARTS],
       chunk_rows[SDF_MAX_DECODE_PARTS], run_gap_rows[SDF_MAX_DECODE_PARTS];
+  // part r's stream at part_ptr[r] when non-null (another device's memory,
+  // peer-mapped: sdf_render_multi), else at parts + r * part_stride
+  const void* part_ptr[SDF_MAX_DECODE_PARTS];
 };
 int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, void* stream);
 

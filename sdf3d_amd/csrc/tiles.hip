@@ -84,7 +84,8 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
   const int tiles_x = (width + 7) >> 3;
   const int ntiles = tiles_x * ((rows + 7) >> 3);
   if (tbase >= ntiles) return;
-  const uint8_t* base = parts + (long long)part * D.part_stride;
+  const uint8_t* base = D.part_ptr[part] ? reinterpret_cast<const uint8_t*>(D.part_ptr[part])
+                                         : parts + (long long)part * D.part_stride;
   const TilesLayout Lt(ntiles);
   const int nt = min(TPW, ntiles - tbase);
   // the header word is loaded with the tables (a part with ntiles = 0 holds

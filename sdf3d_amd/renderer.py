@@ -161,6 +161,31 @@ class Renderer:
         abi.check(rc, "sdf_render")
         return rgba, st
 
+    def render_multi(self, frame: Frame, devices, shares=(0, 0), out=None, stream=None):
+        """One RGBA32F frame rendered across `devices` (device indices of this
+        process, this renderer's device first) through sdf_render_multi: the
+        root renders its rows in place and decodes the other devices' TILES
+        streams through peer-mapped memory.  Returns the (H, W, 4) frame on
+        this renderer's device, asynchronous on `stream`."""
+        torch = self.torch
+        devs = [int(d) for d in devices]
+        if not devs or devs[0] != self.device.index:
+            raise ValueError("devices[0] must be this renderer's device")
+        p = frame.params
+        if out is None:
+            out = torch.empty((p.height, p.width, 4), dtype=torch.float32, device=self.device)
+        if (tuple(out.shape) != (p.height, p.width, 4) or out.dtype != torch.float32
+                or not out.is_contiguous() or out.device != self.device):
+            raise ValueError("out must be a contiguous float32 (H, W, 4) tensor on the root")
+        arr = (C.c_int32 * len(devs))(*devs)
+        with self._on_device():
+            rc = self.lib.sdf_render_multi(
+                C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
+                C.byref(frame.material), C.byref(frame.params), len(devs), arr,
+                int(shares[0]), int(shares[1]), C.c_void_p(out.data_ptr()), self._stream(stream))
+        abi.check(rc, "sdf_render_multi")
+        return out
+
     def heatmap(self, steps, which: int = 0, max_steps: int = 128, fmt: int = abi.FORMAT_RGBA8,
                 out=None, stream=None):
         """Turbo-coloured view of a `steps` tensor (rows, W, 2) from render()."""
