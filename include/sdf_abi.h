@@ -324,7 +324,10 @@ int sdf_owned_rows(int32_t height, const sdf_tiling* tiling);
 int sdf_format_bytes(int32_t format);
 
 /* Capacity in bytes of a TILES stream of `rows` packed rows of `width`
- * pixels (the worst case: 32-bit residuals), or a negative SDF_E* code. */
+ * pixels (the worst case: 32-bit residuals), or a negative SDF_E* code
+ * (SDF_E_UNSUPPORTED when that worst case would not fit the stream's 32-bit
+ * offsets: more than ~5.6M tiles, ~358 Mpixels; sdf_render refuses such a
+ * TILES render the same way). */
 int64_t sdf_tiles_bytes(int32_t width, int32_t rows);
 
 /* Render the rows owned by `tiling` (NULL = whole frame) into `rgba`

@@ -340,6 +340,10 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
   plan->tiles_ntiles = params->output_format == SDF_FORMAT_TILES
                            ? ((params->width + 7) / 8) * ((rows + 7) / 8)
                            : 0;
+  // TILES offsets and the `used` header word are uint32 (tiles.hip): a
+  // stream whose worst case would not fit them is refused, not wrapped
+  if (plan->tiles_ntiles > 0 && TilesLayout(plan->tiles_ntiles).stream_end > 0xffffffffull)
+    return SDF_E_UNSUPPORTED;
   return SDF_OK;
 }
 
@@ -519,6 +523,7 @@ int sdf_format_bytes(int32_t format) {
 int64_t sdf_tiles_bytes(int32_t width, int32_t rows) {
   if (width <= 0 || rows < 0) return SDF_E_INVALID_ARG;
   const int64_t ntiles = int64_t((width + 7) / 8) * ((rows + 7) / 8);
+  if (sdf::TilesLayout(ntiles).stream_end > 0xffffffffull) return SDF_E_UNSUPPORTED;
   return (int64_t)sdf::TilesLayout(ntiles).end;
 }
 
