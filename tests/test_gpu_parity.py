@@ -326,6 +326,14 @@ def test_invalid_arguments_are_rejected_on_device(renderer):
     assert rc == abi.SDF_E_INVALID_ARG
     with pytest.raises(abi.SdfError):
         renderer.render(f, out=out)
+    # a TILES render whose worst-case stream overflows its 32-bit offsets is
+    # refused before any launch
+    g = scenes.reference(65536, 8192)
+    g.params.output_format = abi.FORMAT_TILES
+    rc = lib.sdf_render(C.byref(g.scene), C.byref(g.camera), C.byref(g.light),
+                        C.byref(g.material), C.byref(g.params), None,
+                        C.c_void_p(out.data_ptr()), None, None)
+    assert rc == abi.SDF_E_UNSUPPORTED
 
 
 @pytest.mark.parametrize("fmt", [abi.FORMAT_RGBA16F, abi.FORMAT_RGBA8, abi.FORMAT_RGB32F])
