@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--clock-warm-s", type=float, default=0.3,
                     help="seconds of render launches before anything is measured (the "
                          "GPU's clocks ramp up over ~0.1 s of load)")
-    ap.add_argument("--cpu-sample-stride", type=int, default=4,
+    ap.add_argument("--cpu-sample-stride", type=int, default=1,
                     help="CPU baseline renders every k-th 8-row block of the frame")
     ap.add_argument("--cpu-frames", type=int, default=5)
     ap.add_argument("--no-verify", action="store_true",
@@ -186,25 +186,42 @@ def lib_bpp(frame):
     return abi.load_library().sdf_format_bytes(frame.params.output_format)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(frame, stride, frames):
+    """The CPU oracle (the reference shader restated: its own OpenCL kernel
+    is empty and no CPU OpenCL device exists) on whole frames (stride 1) or
+    every stride-th 8-row block, OpenMP over the host threads this process
+    may use, median of `frames` after one warm-up."""
     import oracle
     from sdf3d_amd import renderer as R
-    t = R.tiling(0, stride, 8)
+    t = R.tiling(0, stride, 8) if stride > 1 else None
     n = oracle.default_threads()
     rows = oracle.owned_rows(frame.params.height, t)
-    oracle.render(frame, t, nthreads=n)          # warm-up
+    oracle.render(frame, t, nthreads=n, variant="baseline")          # warm-up
     times = []
     for _ in range(frames):
         t0 = time.perf_counter()
-        oracle.render(frame, t, nthreads=n)
+        oracle.render(frame, t, nthreads=n, variant="baseline")
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     px = rows * frame.params.width
+    what = ("whole frames" if stride <= 1 else
+            f"every {stride}th 8-row block ({rows} rows, {px} px)")
     return {"value": round(px / med / 1e6, 4), "unit": "Mpixels/s", "cores": n, "kind": "port",
-            "sample": f"{frame.name} {frame.params.width}x{frame.params.height}, every "
-                      f"{stride}th 8-row block ({rows} rows, {px} px), median of {frames} "
-                      f"after 1 warm-up, {n} OpenMP threads, CPU oracle "
-                      f"(oracle/oracle_core.h, -O3 -ffp-contract=off)",
+            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"{frame.name} {frame.params.width}x{frame.params.height}, {what}, "
+                      f"median of {frames} after 1 warm-up, {n} OpenMP threads (the process's "
+                      f"CPU affinity), CPU oracle (oracle/oracle_core.h, gcc -O3 "
+                      f"-march=x86-64-v4 -ffp-contract=off, no fast-math)",
             "seconds_per_sample": round(med, 3)}
 
 

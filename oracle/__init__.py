@@ -26,6 +26,8 @@ LIB_PATH = HERE / "build" / "liboracle.so"
 # the contracted fp32 reading (FMA-fused multiply-adds, which GLSL permits
 # outside `precise`; see oracle/Makefile) -- diagnosis only
 FMA_LIB_PATH = HERE / "build" / "liboracle_fma.so"
+# the CPU-baseline build (x86-64-v4, same IEEE arithmetic; oracle/Makefile)
+BASELINE_LIB_PATH = HERE / "build" / "liboracle_baseline.so"
 _libs = {}
 
 
@@ -37,7 +39,7 @@ def build() -> Path:
 def load(variant: str = "ieee") -> C.CDLL:
     if variant in _libs:
         return _libs[variant]
-    path = {"ieee": LIB_PATH, "fma": FMA_LIB_PATH}[variant]
+    path = {"ieee": LIB_PATH, "fma": FMA_LIB_PATH, "baseline": BASELINE_LIB_PATH}[variant]
     if not path.exists():
         build()
     lib = C.CDLL(str(path))
@@ -126,7 +128,8 @@ def render(frame, t=None, nthreads: int | None = None, twin: bool = False,
 
     Returns (rgba float32 [rows, W, 4], steps int32 [rows, W, 2]).
     `twin=True` runs the fp64 twin (diagnosis only); variant="fma" runs the
-    contracted fp32 reading (diagnosis only)."""
+    contracted fp32 reading (diagnosis only); variant="baseline" the
+    x86-64-v4 build of the IEEE restatement (bench.py's CPU baseline)."""
     lib = load(variant)
     p = frame.params
     rows = owned_rows(p.height, t)

@@ -46,3 +46,17 @@ def test_oracle_threads_deterministic():
     a, sa = oracle.render(f, nthreads=1)
     b, sb = oracle.render(f, nthreads=4)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(sa, sb)
+
+
+def test_baseline_build_is_the_same_oracle():
+    """bench.py's CPU baseline runs the x86-64-v4 build of the oracle
+    (oracle/Makefile): the same IEEE arithmetic, so the same frame bit for
+    bit (skipped on a host without AVX-512)."""
+    import pytest
+    if "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("host CPU lacks AVX-512")
+    from sdf3d_amd import scenes
+    f = scenes.config("C3", 96, 54, pose=1)
+    a, sa = oracle.render(f)
+    b, sb = oracle.render(f, variant="baseline")
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(sa, sb)
