@@ -32,6 +32,7 @@ __global__ __launch_bounds__(256) void deinterleave_rows(const T* __restrict__ p
 int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int row_bytes,
                         int height, int block_rows, void* frame, void* stream) {
   if (height == 0 || row_bytes == 0) return 0;
+  (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   hipStream_t s = (hipStream_t)stream;
   if (row_bytes % 16 == 0) {
     hipLaunchKernelGGL(deinterleave_rows<uint4>, dim3(height), dim3(256), 0, s,
@@ -64,6 +65,7 @@ __global__ __launch_bounds__(256) void deinterleave_rgb_rows(const float* __rest
 int launch_deinterleave_rgb(const void* parts, int nparts, int part_stride_rows, int width,
                             int height, int block_rows, void* frame, void* stream) {
   if (height == 0 || width == 0) return 0;
+  (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   hipLaunchKernelGGL(deinterleave_rgb_rows, dim3(height), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const float*>(parts), nparts, part_stride_rows, width,
                      block_rows, reinterpret_cast<float4*>(frame));

@@ -59,6 +59,7 @@ __global__ __launch_bounds__(256) void heatmap_kernel(const int2* __restrict__ s
 int launch_heatmap(const int32_t* steps, int count, int which, int max_steps, int format,
                    void* out, void* stream) {
   if (count == 0) return 0;
+  (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   hipLaunchKernelGGL(heatmap_kernel, dim3((count + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, reinterpret_cast<const int2*>(steps), count, which,
                      (float)max_steps, format, out);

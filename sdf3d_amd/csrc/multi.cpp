@@ -158,11 +158,10 @@ void default_shares(int n, int* a, int* b) {
 
 }  // namespace
 
-extern "C" int sdf_render_multi(const sdf_scene* scene, const sdf_camera* camera,
-                                const sdf_light* light, const sdf_material* material,
-                                const sdf_params* params, int32_t ndev, const int32_t* devices,
-                                int32_t share_root, int32_t share_peer, void* rgba,
-                                void* stream) {
+static int render_multi(const sdf_scene* scene, const sdf_camera* camera,
+                        const sdf_light* light, const sdf_material* material,
+                        const sdf_params* params, int32_t ndev, const int32_t* devices,
+                        int32_t share_root, int32_t share_peer, void* rgba, void* stream) {
   if (!params || !devices || !rgba || ndev < 1 || ndev > SDF_MAX_DECODE_PARTS)
     return SDF_E_INVALID_ARG;
   if (params->output_format != SDF_FORMAT_RGBA32F) return SDF_E_UNSUPPORTED;
@@ -236,6 +235,19 @@ extern "C" int sdf_render_multi(const sdf_scene* scene, const sdf_camera* camera
     }
   rc = hip_ok((hipError_t)sdf::launch_tiles_decode(c.decode, rgba, nullptr, s));
   if (rc == SDF_OK) rc = hip_ok(hipEventRecord(c.ready[k], s));
+  return rc;
+}
+
+extern "C" int sdf_render_multi(const sdf_scene* scene, const sdf_camera* camera,
+                                const sdf_light* light, const sdf_material* material,
+                                const sdf_params* params, int32_t ndev, const int32_t* devices,
+                                int32_t share_root, int32_t share_peer, void* rgba,
+                                void* stream) {
+  const int rc = render_multi(scene, camera, light, material, params, ndev, devices, share_root,
+                              share_peer, rgba, stream);
+  // HIP keeps the last error per thread: a call refused here must not leave
+  // it for the caller's next, unrelated, check
+  if (rc != SDF_OK) (void)hipGetLastError();
   return rc;
 }
 

@@ -337,6 +337,7 @@ __global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles) {
 
 int launch_tiles_compact(void* stream_buf, int ntiles, void* stream) {
   if (ntiles <= 0) return 0;
+  (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   uint8_t* buf = reinterpret_cast<uint8_t*>(stream_buf);
   hipLaunchKernelGGL(tiles_scan, dim3((ntiles + kScanTiles - 1) / kScanTiles), dim3(256), 0,
                      (hipStream_t)stream, buf, ntiles);
@@ -354,6 +355,7 @@ int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, vo
   const int waves_per_part = (tiles_per_part + kDecodeTiles - 1) / kDecodeTiles;
   const long long waves = (long long)waves_per_part * d.nparts;
   if (waves == 0) return 0;
+  (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   hipLaunchKernelGGL(decode_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, d, reinterpret_cast<const uint8_t*>(parts),
                      waves_per_part, reinterpret_cast<float4*>(frame));

@@ -58,4 +58,7 @@ def test_render_multi_rejects_bad_arguments():
         rd.render_multi(f, [0, 99])          # no such device
     with pytest.raises(ValueError):
         rd.render_multi(f, [1, 0])           # devices[0] must be the renderer's
+    # a refused call leaves no stale HIP error behind for the next launch
+    rd.render(f)
+    torch.cuda.synchronize()
     abi.load_library().sdf_render_multi_release()
