@@ -30,10 +30,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C4")
     ap.add_argument("--pose", type=int, default=0)
+    ap.add_argument("--lib", default=None, help="a prebuilt -DSDF_STATS library (default: build "
+                                               "sdf3d_amd/lib/libsdf3d_stats.so)")
+    ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import torch
     from sdf3d_amd import Renderer, abi, build, scenes
-    lib = abi.load_library(build.build_stats_library(verbose=False))
+    lib = abi.load_library(args.lib or build.build_stats_library(verbose=False))
     lib.sdf_debug_stats.restype = C.c_int
     lib.sdf_debug_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     rd = Renderer("cuda:0")
@@ -60,8 +63,12 @@ def main():
             "prim_cached_skip": [round(x, 3) for x in v[4:12]],
             "prim_fresh_test": [round(x, 3) for x in v[12:20]],
             "prim_evaluated": [round(x, 3) for x in v[20:28]],
+            "prim_fresh_total": round(sum(v[12:20]), 3),
+            "prim_evaluated_total": round(sum(v[20:28]), 3),
         }
     print(json.dumps(out, indent=1))
+    if args.out:
+        Path(args.out).write_text(json.dumps(out, indent=1) + "\n")
 
 
 if __name__ == "__main__":
