@@ -56,7 +56,8 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 7   /* 7: sdf_comm_create timeout, sdf_render_multi */
+#define SDF_ABI_VERSION 8   /* 7: sdf_comm_create timeout, sdf_render_multi;
+                                8: sdf_render_frames */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -481,6 +482,23 @@ int sdf_render_multi(const sdf_scene* scene, const sdf_camera* camera, const sdf
                      void* stream);
 /* Wait for and free the buffers sdf_render_multi keeps. */
 int sdf_render_multi_release(void);
+
+/* ---- frame sequences ----------------------------------------------------------
+ * n whole frames of one scene: frame i seen through cameras[i], written to
+ * rgba[i] (width * height pixels of params->output_format; TILES is
+ * SDF_E_UNSUPPORTED) and, when `steps` is non-null and steps[i] is, its
+ * iteration counts to steps[i] (width * height int2).  Equal bit for bit to
+ * n sdf_render calls with the same arguments.  This is the reference's frame
+ * loop (main.cpp:87-98) for a camera path known in advance: the frames are
+ * rendered by a persistent kernel, up to 16 frames per launch, whose waves
+ * take 8x8 tiles of all its frames from one work counter, so a frame's
+ * slowest tiles overlap the next frame's first ones.  Asynchronous on
+ * `stream` (a stream of the current device).  Every camera is validated
+ * before anything is enqueued. */
+int sdf_render_frames(const sdf_scene* scene, const sdf_camera* cameras, int32_t n,
+                      const sdf_light* light, const sdf_material* material,
+                      const sdf_params* params, void* const* rgba, int32_t* const* steps,
+                      void* stream);
 
 /* Short description of a status code. */
 const char* sdf_strerror(int code);

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 7
+SDF_ABI_VERSION = 8
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -132,6 +132,9 @@ SIGNATURES = {
                                    _P(sdf_material), _P(sdf_params), C.c_int32, C.c_void_p,
                                    C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_render_multi_release": (C.c_int, []),
+    "sdf_render_frames": (C.c_int, [_P(sdf_scene), _P(sdf_camera), C.c_int32, _P(sdf_light),
+                                    _P(sdf_material), _P(sdf_params), C.c_void_p, C.c_void_p,
+                                    C.c_void_p]),
     "sdf_comm_unique_id": (C.c_int, [C.c_char_p, C.c_void_p]),
     "sdf_comm_create": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                   _P(C.c_void_p)]),

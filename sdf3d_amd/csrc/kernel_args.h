@@ -66,11 +66,49 @@ struct KernelArgs {
   int32_t* steps;       // rows * width int2 or null
 };
 
+// ---- frame sequences (sdf_render_frames) ----------------------------------
+// Up to kFramesPerLaunch whole frames of one scene in one launch of a
+// persistent kernel: its waves take 8x8 tiles of all the launch's frames from
+// one work counter, frame after frame, so a frame's slowest tiles overlap the
+// next frame's first ones instead of ending a launch.  The per-frame uniforms
+// ride in the kernel-argument segment beside the shared KernelArgs (whose own
+// camera and output fields are unused): 1,872 + 16 x 104 bytes.
+constexpr int kFramesPerLaunch = 16;
+struct FrameCam {
+  float inv_view[16];   // inverse(V_mat) of this frame's camera
+  float cam[3];
+  float focal, aspect;
+  void* rgba;           // width * height pixels of the params' format
+  int32_t* steps;       // width * height int2 or null
+};
+struct FramesArgs {
+  KernelArgs a;
+  FrameCam frame[kFramesPerLaunch];
+  int32_t nframes;          // 1 .. kFramesPerLaunch
+  int32_t tiles_x;          // ceil(width / 8)
+  int32_t tiles_per_frame;  // tiles_x * ceil(height / 8)
+  int32_t queues;           // work queues (1 .. kFrameQueues, <= workgroups)
+  int32_t schedule;         // 0 work queues, 1 static (tools/frames_probe.py)
+  int32_t chunk;            // tiles per queue request (kChunkTiles)
+  uint32_t* counter;        // queue q's counter at counter[q * kQueueStride], zero at launch
+};
+// Tiles a wave takes per queue request, queues per launch (workgroup b uses
+// queue b % queues, i.e. one per XCD), and the queues' spacing in uint32s:
+// requests on one address serialise at the memory-side atomic unit, so the
+// launch spreads them over several addresses and asks for 2 tiles at a time.
+constexpr int kChunkTiles = 2;
+constexpr int kFrameQueues = 32;   // at most; kDefaultQueues by default
+constexpr int kDefaultQueues = 8;
+constexpr int kQueueStride = 64;
+
 // Kernel launchers, one per precision translation unit (render_exact.hip /
 // render_fast.hip); `variant` selects a compile-time scene specialisation
 // (see render_kernel.inc).  Return a hipError_t as int.
 int launch_render_exact(const KernelArgs& a, int variant, void* stream);
 int launch_render_fast(const KernelArgs& a, int variant, void* stream);
+// the persistent frame-sequence kernel on `nblocks` 256-thread workgroups
+int launch_frames_exact(const FramesArgs& a, int variant, int nblocks, void* stream);
+int launch_frames_fast(const FramesArgs& a, int variant, int nblocks, void* stream);
 int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int row_bytes,
                         int height, int block_rows, void* frame, void* stream);
 int launch_heatmap(const int32_t* steps, int count, int which, int max_steps, int format,

@@ -186,6 +186,38 @@ class Renderer:
         abi.check(rc, "sdf_render_multi")
         return out
 
+    def render_frames(self, frame: Frame, cameras, outs, steps=None, stream=None):
+        """Whole frames of `frame`'s scene, frame i through cameras[i] into
+        outs[i] (and its iteration counts into steps[i]), by the persistent
+        frame-sequence kernel (sdf_render_frames): the same pixels as one
+        ``render`` per camera.  Asynchronous on `stream`; returns `outs`."""
+        torch = self.torch
+        n = len(cameras)
+        if len(outs) != n or (steps is not None and len(steps) != n):
+            raise ValueError("one output (and one steps buffer) per camera")
+        p = frame.params
+        if p.output_format == abi.FORMAT_TILES:
+            raise ValueError("frame sequences take plain formats, not TILES")
+        dt, ch = torch_dtype(p.output_format), channels(p.output_format)
+        for o in outs:
+            if tuple(o.shape) != (p.height, p.width, ch) or o.dtype != dt \
+                    or not o.is_contiguous() or o.device != self.device:
+                raise ValueError(f"outputs must be contiguous {dt} ({p.height}, {p.width}, {ch}) "
+                                 f"tensors on {self.device}")
+        for s in steps or ():
+            if tuple(s.shape) != (p.height, p.width, 2) or s.dtype != torch.int32 \
+                    or not s.is_contiguous() or s.device != self.device:
+                raise ValueError("steps must be contiguous int32 (H, W, 2) tensors")
+        cams = (abi.sdf_camera * max(n, 1))(*cameras)
+        ptrs = (C.c_void_p * max(n, 1))(*[o.data_ptr() for o in outs])
+        sptrs = (C.c_void_p * max(n, 1))(*[s.data_ptr() for s in steps]) if steps else None
+        with self._on_device():
+            rc = self.lib.sdf_render_frames(
+                C.byref(frame.scene), cams, n, C.byref(frame.light), C.byref(frame.material),
+                C.byref(frame.params), ptrs, sptrs, self._stream(stream))
+        abi.check(rc, "sdf_render_frames")
+        return outs
+
     def heatmap(self, steps, which: int = 0, max_steps: int = 128, fmt: int = abi.FORMAT_RGBA8,
                 out=None, stream=None):
         """Turbo-coloured view of a `steps` tensor (rows, W, 2) from render()."""
