@@ -429,6 +429,22 @@ inline void render_multi(const Frame& f, const std::vector<int>& devices, float*
         "sdf_render_multi");
 }
 
+// A camera path known in advance (sdf_render_frames): frame i of `f`'s scene
+// seen through cameras[i] into rgba[i] (steps[i] when `steps` is non-empty),
+// by the persistent frame-sequence kernel; the pixels of one sdf_render per
+// camera.  Asynchronous on `stream`.
+inline void render_frames(const Frame& f, const std::vector<sdf_camera>& cameras,
+                          const std::vector<void*>& rgba, hipStream_t stream,
+                          const std::vector<int32_t*>& steps = {}) {
+  check_abi();
+  if (rgba.size() != cameras.size() || (!steps.empty() && steps.size() != cameras.size()))
+    throw Error(SDF_E_INVALID_ARG, "render_frames: one output per camera");
+  check(sdf_render_frames(&f.scene, cameras.data(), static_cast<int32_t>(cameras.size()),
+                          &f.light, &f.material, &f.params, rgba.data(),
+                          steps.empty() ? nullptr : steps.data(), stream),
+        "sdf_render_frames");
+}
+
 // Binary PPM of an RGBA float framebuffer, clamped and quantised to 8 bits
 // (what the reference's window would show), flipped to top-down row order.
 inline void write_ppm(const std::string& path, const std::vector<float>& rgba, int w, int h) {
