@@ -42,6 +42,7 @@ struct KernelArgs {
   int32_t ao_taps;
   float ao_step, ao_base, ao_falloff, ao_strength;
   float ao_h[kMaxAoTaps];  // tap heights base + step * i / (taps - 1), host fp32
+  float ao_path[kMaxAoTaps];  // path length P -> tap 0 -> .. -> tap i (fp64, rounded up)
   float inv_width, inv_height;  // fast precision quad mapping
   // tiling
   int32_t block_rows, first_block, block_stride, rows;

@@ -308,6 +308,17 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
     const float tt = a.ao_taps > 1 ? (float)i / (float)(a.ao_taps - 1) : 0.0f;
     a.ao_h[i] = params->ao_base + params->ao_step * tt;
   }
+  // the AO taps' path lengths from P, visited in order (render_kernel.inc):
+  // |h_0| + sum |h_k - h_(k-1)|, rounded up to fp32 so it never undercounts
+  {
+    double path = 0.0;
+    for (int i = 0; i < a.ao_taps && i < kMaxAoTaps; ++i) {
+      path += std::fabs((double)a.ao_h[i] - (i ? (double)a.ao_h[i - 1] : 0.0));
+      float f = (float)path;
+      if ((double)f < path) f = std::nextafter(f, INFINITY);
+      a.ao_path[i] = f;
+    }
+  }
   a.inv_width = 1.0f / (float)params->width;
   a.inv_height = 1.0f / (float)params->height;
   a.block_rows = t.block_rows;

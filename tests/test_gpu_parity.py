@@ -569,6 +569,27 @@ def test_culling_exact_on_random_scenes(renderer, seed):
     assert_parity(report(c, sc, b, sb), what=f"seed {seed} generic")
 
 
+@pytest.mark.parametrize("normal_mode,h,ao_base,ao_step", [
+    (abi.NORMAL_TETRA, -0.01, -0.01, -0.12), (abi.NORMAL_CENTRAL, -0.02, 0.3, -0.2),
+    (abi.NORMAL_TETRA, 0.05, -0.4, 0.1)])
+def test_culling_exact_with_negative_offsets(renderer, normal_mode, h, ao_base, ao_step):
+    """Negative normal_eps / AO offsets are valid parameters (sdf_validate
+    accepts any finite value): the culled kernel's path lengths for the
+    normal and AO taps use |h|, so it still equals the unculled kernel bit for
+    bit (exact precision), step counts included."""
+    f = random_csg8(np.random.default_rng(7), 1.0, 0.3)
+    f.params.normal_mode = normal_mode
+    f.params.normal_eps = h
+    f.params.ao_base, f.params.ao_step = ao_base, ao_step
+    f.params.precision = abi.PRECISION_EXACT
+    a, sa = gpu(renderer, f)
+    u = f.copy()
+    u.params.dispatch = abi.DISPATCH_UNCULLED
+    b, sb = gpu(renderer, u)
+    assert np.array_equal(sa, sb)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 @pytest.mark.parametrize("peer_root", [False, True])
 def test_cpp_frame_driver(renderer, tmp_path, peer_root):
     """The C++ host program's native frame-driver mode (sdf::FrameDriver over
