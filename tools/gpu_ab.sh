@@ -11,6 +11,8 @@ export TMPDIR=/tmp
 TESTS=${TESTS:-tests}
 POSES=${POSES:-0,1,2,3}
 CONFIGS=${CONFIGS:-C4}
+# name=path pairs; bit-exactness is reported against the first
+LIBS=${LIBS:-base=tools/_variants/libsdf3d_base.so new=sdf3d_amd/lib/libsdf3d.so}
 if [ "$TESTS" != none ]; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q -rf --timeout 300 \
     --timeout-method thread > gpurun_out/ab_pytest.log 2>&1
@@ -18,8 +20,7 @@ if [ "$TESTS" != none ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 for c in $CONFIGS; do
-  timeout -k 10 300 python tools/ab_kernel.py base=tools/_variants/libsdf3d_base.so \
-    new=sdf3d_amd/lib/libsdf3d.so --config $c --poses $POSES --out gpurun_out/ab_$c.json \
+  timeout -k 10 300 python tools/ab_kernel.py $LIBS --config $c --poses $POSES --out gpurun_out/ab_$c.json \
     > gpurun_out/ab_$c.log 2>&1
   rc=$?; echo "ab $c rc=$rc"; cat gpurun_out/ab_$c.log | grep '^{'
   [ $rc -ne 0 ] && exit $rc
