@@ -2,10 +2,13 @@
 
 Exact precision (IEEE div/sqrt, no contraction) must satisfy the parity policy
 of tests/parity.py against the golden fixtures and fresh oracle renders; fast
-precision (hardware sqrt/rcp, FMA) is held to the same policy.  Full-size
-(BASELINE) frames are checked through size-independent properties: step-count
-sums against the oracle's full-frame statistics, determinism, tiling
-invariance, finiteness.
+precision (hardware sqrt/rcp, FMA) is held to the same policy, or, on
+fp32-ill-conditioned frames, to the spread of the oracle's own alternative
+readings (check_frame).  Full-size (BASELINE) frames are compared per pixel
+with a live oracle render on the bench's own code path
+(test_full_size_pixel_parity), and through size-independent properties:
+step-count sums against the oracle's full-frame statistics, determinism,
+tiling invariance, finiteness.
 """
 import ctypes as C
 import json
@@ -275,13 +278,14 @@ def test_full_size_properties(renderer, cfg, prec):
 
 
 FULL_CASES = [("C4", abi.PRECISION_FAST), ("C4", abi.PRECISION_EXACT),
+              ("C3", abi.PRECISION_FAST), ("C3", abi.PRECISION_EXACT),
               ("C2", abi.PRECISION_FAST), ("C2", abi.PRECISION_EXACT),
               ("C5", abi.PRECISION_FAST), ("C5", abi.PRECISION_EXACT)]
 
 
 @pytest.mark.parametrize("cfg,prec", FULL_CASES)
 def test_full_size_pixel_parity(renderer, cfg, prec):
-    """Per-pixel parity at the BASELINE size (C4/C5 3840x2160, C2 1920x1080)
+    """Per-pixel parity at the BASELINE size (C4/C5 3840x2160, C3/C2 1920x1080)
     on the bench's own code path: the frame rendered WITHOUT a steps buffer
     (exact shadow skip active), against a live oracle render of the same
     frame on all host threads (voxel_fragment.frag:160-211), under
