@@ -40,6 +40,23 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parent
+
+# Hardware queues per process for HIP streams (read at HIP initialisation,
+# before torch touches the GPU).  The frame driver keeps 3-4 render streams
+# plus 2 communication streams; with HIP's default of 4 hardware queues some
+# of them share a queue, whose FIFO order serialises their kernels: on one
+# MI355X a rank-sized TILES share on 4 alternating streams took 0.073 ms per
+# frame with 4 queues and 0.057 with 8 (tools/root_probe.py --streams,
+# profiles/r02_hw_queues_C4.json).  A value set by the caller wins.  Not
+# for the gloo rehearsals, whose ranks all share one GPU (up to 8 processes:
+# HIP's default keeps their queue count at what one GPU was tested with).
+def _gloo_rehearsal(argv):
+    return any(a == "--backend=gloo" or (a == "--backend" and argv[i + 1:i + 2] == ["gloo"])
+               for i, a in enumerate(argv))
+
+
+if not _gloo_rehearsal(sys.argv[1:]):
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mpixels/s (primary+shadow+AO) at 3840×2160, 1/2/4/8 MI355X"

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--shares", default="1:1", help="rank 0 : other ranks, blocks per period")
+    ap.add_argument("--streams", type=int, default=3, help="alternating streams / buffers")
     ap.add_argument("--only", choices=["decode", "root", "peer"], default=None,
                     help="time one leg only (for rocprofv3 counter passes)")
     args = ap.parse_args()
@@ -51,16 +52,17 @@ def main():
     parts = torch.zeros(N * stride, dtype=torch.uint8, device=rd.device)
     for r in range(1, N):
         rd.render(ft, tilings[r], out=parts[r * stride:(r + 1) * stride])
-    frames = [torch.empty((H, W, 4), dtype=torch.float32, device=rd.device) for _ in range(3)]
-    streams = [torch.cuda.Stream() for _ in range(3)]
+    NS = args.streams
+    frames = [torch.empty((H, W, 4), dtype=torch.float32, device=rd.device) for _ in range(NS)]
+    streams = [torch.cuda.Stream() for _ in range(NS)]
     side = torch.cuda.Stream()
     t0_tiling = R.tiling(0, N, 8, frame_rows=True, shares=shares)
     # the busiest peer: the most rows
     busiest = max(range(1, N), key=lambda r: R.owned_rows(H, tilings[r])) if N > 1 else 0
-    peer_bufs = [torch.empty(stride, dtype=torch.uint8, device=rd.device) for _ in range(3)]
+    peer_bufs = [torch.empty(stride, dtype=torch.uint8, device=rd.device) for _ in range(NS)]
 
     def run(render=True, decode=True, serial=False, peer=False):
-        for b in range(3):
+        for b in range(NS):
             if peer:
                 rd.render(ft, tilings[busiest], out=peer_bufs[b], stream=streams[b])
             if render:
@@ -71,7 +73,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(K):
-            b = i % 3
+            b = i % NS
             s = streams[b]
             if peer:
                 rd.render(ft, tilings[busiest], out=peer_bufs[b], stream=s)
@@ -86,15 +88,15 @@ def main():
 
     def fill():
         for i in range(K):
-            frames[i % 3].fill_(1.0)
+            frames[i % NS].fill_(1.0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(K):
-            frames[i % 3].fill_(1.0)
+            frames[i % NS].fill_(1.0)
         torch.cuda.synchronize()
         return round((time.perf_counter() - t0) / K * 1e3, 4)
 
-    out = {"config": args.config, "world": N, "shares": args.shares, "frames": K}
+    out = {"config": args.config, "world": N, "shares": args.shares, "frames": K, "streams": NS}
     if args.only:
         leg = {"decode": dict(render=False), "root": dict(), "peer": dict(render=False,
                decode=False, peer=True)}[args.only]
