@@ -9,9 +9,10 @@ ranks (one process per GPU, torchrun) each rank renders its interleaved 8-row
 blocks of the frame (rank 0 fewer: multigpu.choose_shares); the peers ship
 them as lossless TILES streams to rank 0 over RCCL, and rank 0 decodes them
 straight into the frame (sdf_tiles_decode_tilings).  Frames are pipelined
-over 4 buffer sets on alternating streams: frame i ships while frames i+1,
-i+2 render.  Total work per step is one frame whatever N is ("scaling":
-"strong").
+over 4 buffer sets on alternating streams (3 at N = 1): frame i ships while
+frames i+1, i+2 render; HIP gets 8 hardware queues so that those streams do
+not share one (GPU_MAX_HW_QUEUES, below).  Total work per step is one frame
+whatever N is ("scaling": "strong").
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C4]
                     [--precision fast|exact] [--no-cpu-baseline]
@@ -23,9 +24,10 @@ summary, profiles/pmc_<cfg>_<prec>.json) over the kernel's average duration
 measured with HIP events on the launch stream, against the 157.3 TFLOP/s FP32
 vector peak, with the counter-based VALU busy of the same PMC run and, as
 `alg_equiv`, the SURVEY.md 8(d) algorithmic count (oracle step counts in
-tests/golden/stats_<cfg>_p0.npz) over the same time (see roofline()).  `cpu_baseline` times the CPU oracle (a restatement of the reference
-shader: the reference's own OpenCL kernel is empty and no CPU OpenCL device
-exists) on a bounded sample of the same frame, rank 0 at N=1 only.
+tests/golden/stats_<cfg>_p0.npz) over the same time (see roofline()).
+`cpu_baseline` times the CPU oracle (a restatement of the reference shader:
+the reference's own OpenCL kernel is empty and no CPU OpenCL device exists)
+on whole frames of the same workload, rank 0 at N=1 only.
 """
 from __future__ import annotations
 
