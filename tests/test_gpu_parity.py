@@ -573,6 +573,43 @@ def test_culling_exact_on_random_scenes(renderer, seed):
     assert_parity(report(c, sc, b, sb), what=f"seed {seed} generic")
 
 
+@pytest.mark.parametrize("light,k", [
+    ((5.0, 5.0, 0.0), 10.0),      # the reference's light: slopes b ~ 0.5-0.8
+    ((0.3, 40.0, 0.2), 10.0),     # nearly overhead: b above the 0.95 cap
+    ((-6.0, 0.75, 2.0), 10.0),    # low light: b around the lim >= 1.01 threshold
+    ((4.0, 2.0, -3.0), 2.0),      # soft k: lim < 1 for most slopes
+    ((4.0, 2.0, -3.0), 60.0),     # hard k
+    ((0.0, 0.3, -0.1), 10.0),     # light inside the cluster sphere
+    ((3.0, -1.0, 0.0), 10.0),     # light below the plane: b < 0
+])
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+def test_shadow_lit_tail_exact(renderer, light, k, prec):
+    """The shadow march's lit tail (FixedScene::shadow_limit) ends the march
+    early only on the no-steps path; it must not change one output bit.  gpu()
+    asserts the no-steps frame equals the steps-on frame (full march) bit for
+    bit, here over light positions that put the ray slopes on both sides of
+    every condition, four poses, random CSG8 scenes and a tilted plane (a
+    run-time specialised kernel with sd_plane as head).  Exact precision is
+    also bit-exact with the oracle."""
+    frames = [scenes.config("C3", 240, 136, pose=p) for p in range(4)]
+    frames += [random_csg8(np.random.default_rng(s), 1.0, 0.3) for s in (3, 4)]
+    tilt = scenes.config("C3", 240, 136)
+    n = np.array([0.12, 1.0, -0.05]) / np.linalg.norm([0.12, 1.0, -0.05])
+    tilt.scene.prims[0].kind = abi.PRIM_PLANE
+    tilt.scene.prims[0].p[0], tilt.scene.prims[0].p[1], tilt.scene.prims[0].p[2] = (
+        float(n[0]), float(n[1]), float(n[2]))
+    frames.append(tilt)
+    for i, f in enumerate(frames):
+        f.light.pos[0], f.light.pos[1], f.light.pos[2] = light
+        f.params.shadow_k = k
+        f.params.precision = prec
+        rgba, st = gpu(renderer, f)
+        if prec == abi.PRECISION_EXACT:
+            ref, ref_st = oracle.render(f)
+            assert np.array_equal(st, ref_st), f"frame {i}: step counts"
+            assert np.array_equal(rgba.view(np.uint32), ref.view(np.uint32)), f"frame {i}"
+
+
 @pytest.mark.parametrize("normal_mode,h,ao_base,ao_step", [
     (abi.NORMAL_TETRA, -0.01, -0.01, -0.12), (abi.NORMAL_CENTRAL, -0.02, 0.3, -0.2),
     (abi.NORMAL_TETRA, 0.05, -0.4, 0.1)])
