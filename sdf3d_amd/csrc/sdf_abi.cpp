@@ -151,6 +151,75 @@ void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
   }
 }
 
+// A small sphere containing the n spheres (c_i, r_i): the centre C minimises
+// RC(C) = max_i |c_i - C| + r_i, which is convex in C.  Any C gives a valid
+// bound; the search only makes it tighter (subgradient steps towards the
+// farthest sphere with diminishing length from the centroid, and the
+// two-sphere balls of every pair, keeping the best).  The tighter the
+// cluster sphere, the more often the culling and the shadow march's lit
+// tail (render_kernel.inc) skip it.  Cached per primitive list: sdf_render
+// prepares a plan per call.
+static double sphere_radius_at(const double (*c)[3], const double* r, int n, const double* C) {
+  double R = 0;
+  for (int i = 0; i < n; ++i) {
+    const double dx = c[i][0] - C[0], dy = c[i][1] - C[1], dz = c[i][2] - C[2];
+    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + r[i]);
+  }
+  return R;
+}
+static double cluster_sphere(const double (*c)[3], const double* r, int n, double* C) {
+  thread_local double key[SDF_MAX_PRIMS * 4 + 1] = {-1};
+  thread_local double kC[3], kR = 0;
+  double k[SDF_MAX_PRIMS * 4 + 1] = {(double)n};
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < 3; ++j) k[1 + 4 * i + j] = c[i][j];
+    k[4 + 4 * i] = r[i];
+  }
+  if (std::memcmp(k, key, sizeof(double) * (1 + 4 * n)) == 0) {
+    std::memcpy(C, kC, sizeof(kC));
+    return kR;
+  }
+  double B[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 3; ++j) B[j] += c[i][j] / n;
+  double RB = sphere_radius_at(c, r, n, B);
+  // the ball of each pair, through both spheres' far points
+  for (int i = 0; i < n; ++i)
+    for (int m = i + 1; m < n; ++m) {
+      double u[3], L = 0;
+      for (int j = 0; j < 3; ++j) { u[j] = c[m][j] - c[i][j]; L += u[j] * u[j]; }
+      L = std::sqrt(L);
+      if (!(L > 0)) continue;
+      const double off = 0.5 * (L + r[m] - r[i]);
+      double T[3];
+      for (int j = 0; j < 3; ++j) T[j] = c[i][j] + u[j] / L * off;
+      const double RT = sphere_radius_at(c, r, n, T);
+      if (RT < RB) { RB = RT; std::memcpy(B, T, sizeof(B)); }
+    }
+  // subgradient descent from the best so far
+  double X[3];
+  std::memcpy(X, B, sizeof(X));
+  const double step0 = 0.25 * RB;
+  for (int it = 0; it < 2000; ++it) {
+    int far = 0;
+    double best = -1, dist = 0;
+    for (int i = 0; i < n; ++i) {
+      const double dx = c[i][0] - X[0], dy = c[i][1] - X[1], dz = c[i][2] - X[2];
+      const double d = std::sqrt(dx * dx + dy * dy + dz * dz);
+      if (d + r[i] > best) { best = d + r[i]; far = i; dist = d; }
+    }
+    if (best < RB) { RB = best; std::memcpy(B, X, sizeof(B)); }
+    if (!(dist > 0)) break;
+    const double h = step0 / (1.0 + it);
+    for (int j = 0; j < 3; ++j) X[j] += (c[far][j] - X[j]) / dist * h;
+  }
+  std::memcpy(key, k, sizeof(double) * (1 + 4 * n));
+  std::memcpy(kC, B, sizeof(kC));
+  kR = RB;
+  std::memcpy(C, B, sizeof(kC));
+  return RB;
+}
+
 // Bounding spheres and the cluster bound read by the fixed-scene kernels'
 // culling (kernel_args.h "exact bounding-volume culling").  Radii are computed
 // in double and rounded up.
@@ -191,15 +260,13 @@ void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
   while (first > 0 && cull[first - 1]) --first;
   a.cluster_first = first;
   if (first < s.count) {
-    double C[3] = {0, 0, 0};
+    double C[3];
+    cluster_sphere(cen + first, rad + first, s.count - first, C);
+    for (int j = 0; j < 3; ++j) C[j] = double(float(C[j]));   // the centre the kernel reads
+    const double RC = sphere_radius_at(cen + first, rad + first, s.count - first, C);
+    double kmax = 0;
     for (int i = first; i < s.count; ++i)
-      for (int j = 0; j < 3; ++j) C[j] += cen[i][j] / (s.count - first);
-    double RC = 0, kmax = 0;
-    for (int i = first; i < s.count; ++i) {
-      const double dx = cen[i][0] - C[0], dy = cen[i][1] - C[1], dz = cen[i][2] - C[2];
-      RC = std::max(RC, std::sqrt(dx * dx + dy * dy + dz * dz) + rad[i]);
       if (s.prims[i].op == SDF_OP_SMOOTH_UNION) kmax = std::max(kmax, double(s.prims[i].k));
-    }
     for (int j = 0; j < 3; ++j) a.cluster[j] = float(C[j]);
     a.cluster[3] = float((kmax + RC * (1.0 + 1e-6) + 1e-6 + sdf::kCullAbs) /
                          (1.0 - sdf::kCullRel) * (1.0 + 1e-6));
