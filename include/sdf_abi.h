@@ -385,6 +385,17 @@ int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_
  * SDF_DISPATCH_AUTO). */
 int sdf_jit_count(void);
 
+/* The culling bounds a primitive scene's fixed-scene kernels read (host
+ * only, no device needed; diagnostics and tests): per primitive
+ * bounds[4 * i ..] = {centre.xyz, K_i = (k_i + R_i + 1e-4) / (1 - 1e-5)}
+ * with R_i the radius of a sphere containing primitive i, the cluster
+ * cluster[0..3] = {centre.xyz, K} of the sphere containing primitives
+ * [*cluster_first, count) (K with the largest blend radius), and
+ * *cluster_first (= count when nothing is culled).  bounds holds
+ * 4 * SDF_MAX_PRIMS floats.  SDF_E_UNSUPPORTED for a Mandelbulb scene. */
+int sdf_scene_bounds(const sdf_scene* scene, float* bounds, float* cluster,
+                     int32_t* cluster_first);
+
 /* ---- multi-device frame driver ----------------------------------------------
  * One process per GPU.  Every rank renders its row blocks of each frame
  * (tiling with shares: rank 0 `share_root` blocks and every other rank

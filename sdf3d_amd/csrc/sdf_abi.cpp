@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstring>
 #include <initializer_list>
+#include <memory>
 
 #include "../../include/sdf_abi.h"
 #include "host_api.h"
@@ -616,6 +617,25 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
 }
 
 int sdf_jit_count(void) { return sdf::jit_compiled_count(); }
+
+int sdf_scene_bounds(const sdf_scene* scene, float* bounds, float* cluster,
+                     int32_t* cluster_first) {
+  if (!scene || !bounds || !cluster || !cluster_first) return SDF_E_INVALID_ARG;
+  sdf_camera c;
+  sdf_light l;
+  sdf_material m;
+  sdf_params p;
+  sdf_defaults(nullptr, &c, &l, &m, &p, 0, 0);
+  const int rc = sdf_validate(scene, &c, &l, &m, &p, nullptr);   // the scene's own checks
+  if (rc != SDF_OK) return rc;
+  if (scene->kind != SDF_SCENE_PRIMITIVES) return SDF_E_UNSUPPORTED;
+  std::unique_ptr<sdf::KernelArgs> a(new sdf::KernelArgs());
+  prepare_bounds(*scene, *a);
+  std::memcpy(bounds, a->bound, sizeof(a->bound));
+  std::memcpy(cluster, a->cluster, sizeof(a->cluster));
+  *cluster_first = a->cluster_first;
+  return SDF_OK;
+}
 
 int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_stride,
                              const sdf_tiling* tilings, int32_t width, int32_t height,

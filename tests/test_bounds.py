@@ -1,0 +1,147 @@
+"""Host-side culling bounds (no GPU): sdf_scene_bounds returns the bounding
+spheres the fixed-scene kernels cull with (sdf_abi.cpp prepare_bounds).  Exact
+culling is only exact if every primitive lies inside its own sphere and every
+cullable primitive inside the cluster sphere; these tests restate each
+kind's radius independently and check the containment, and that the cluster
+sphere (a minimax centre since round 2) is never larger than the centroid
+one it replaced (render_kernel.inc: the smaller it is, the more the culling
+and the shadow march's lit tail skip)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from sdf3d_amd import abi, scenes
+
+ABS, REL = 1e-4, 1e-5
+SMOOTH = (abi.OP_SMOOTH_UNION,)
+
+
+def bounds_of(scene):
+    lib = abi.load_library()
+    b = (C.c_float * (4 * abi.SDF_MAX_PRIMS))()
+    c = (C.c_float * 4)()
+    first = C.c_int32()
+    rc = lib.sdf_scene_bounds(C.byref(scene), b, c, C.byref(first))
+    return rc, np.array(b, dtype=np.float64).reshape(-1, 4), np.array(c, dtype=np.float64), first.value
+
+
+def sphere_of(pr):
+    """Centre and radius of a sphere containing the primitive (its own
+    statement of the shapes in render_kernel.inc)."""
+    p = np.array(pr.p, dtype=np.float64)
+    c = p[0:3].copy()
+    if pr.kind == abi.PRIM_SPHERE:
+        r = p[3]
+    elif pr.kind in (abi.PRIM_BOX, abi.PRIM_ROUND_BOX):
+        r = np.linalg.norm(p[3:6])
+    elif pr.kind == abi.PRIM_TORUS:
+        r = p[3] + p[4]
+    elif pr.kind == abi.PRIM_CAPSULE:
+        c = 0.5 * (p[0:3] + p[3:6])
+        r = 0.5 * np.linalg.norm(p[3:6] - p[0:3]) + p[6]
+    elif pr.kind == abi.PRIM_CYLINDER:
+        r = np.hypot(p[3], p[4])
+    else:
+        r = 0.0
+    return c, abs(r)
+
+
+def random_scene(rng, n):
+    f = scenes.config("C3", 64, 64)
+    s = f.scene
+    C.memset(C.addressof(s.prims), 0, C.sizeof(s.prims))
+    s.count = n
+    u = lambda a, b: float(rng.uniform(a, b))  # noqa: E731
+    s.prims[0].kind, s.prims[0].op = abi.PRIM_PLANE, abi.OP_UNION
+    s.prims[0].p[1] = 1.0
+    kinds = [abi.PRIM_SPHERE, abi.PRIM_BOX, abi.PRIM_ROUND_BOX, abi.PRIM_TORUS,
+             abi.PRIM_CAPSULE, abi.PRIM_CYLINDER]
+    for i in range(1, n):
+        pr = s.prims[i]
+        pr.kind = kinds[int(rng.integers(len(kinds)))]
+        pr.op = abi.OP_SMOOTH_UNION if rng.random() < 0.8 else abi.OP_UNION
+        pr.k = u(1e-3, 0.5)
+        for j in range(3):
+            pr.p[j] = u(-3, 3)
+        if pr.kind == abi.PRIM_CAPSULE:
+            for j in range(3, 6):
+                pr.p[j] = u(-3, 3)
+            pr.p[6] = u(0.01, 0.5)
+        else:
+            for j in range(3, 6):
+                pr.p[j] = u(0.01, 1.0)
+            pr.p[6] = u(0.0, 0.05)
+    return f.scene
+
+
+def check_containment(scene):
+    rc, b, cl, first = bounds_of(scene)
+    assert rc == 0
+    n = scene.count
+    centres, radii, ks = [], [], []
+    for i in range(n):
+        pr = scene.prims[i]
+        c, r = sphere_of(pr)
+        k = pr.k if pr.op in SMOOTH else 0.0
+        if i >= first:
+            # the kernel's per-primitive bound: K_i >= (k + R + abs) / (1 - rel)
+            assert np.allclose(b[i, :3], c, rtol=0, atol=1e-6 * (1 + np.abs(c))), i
+            assert b[i, 3] >= (k + r + ABS) / (1 - REL) * (1 - 1e-6), i
+            centres.append(c)
+            radii.append(r)
+            ks.append(k)
+    if first >= n:
+        return None
+    centres, radii = np.array(centres), np.array(radii)
+    kmax = max(ks)
+    rc_cluster = cl[3] * (1 - REL) - ABS - kmax   # the radius the cluster bound encloses
+    far = np.linalg.norm(centres - cl[:3], axis=1) + radii
+    assert np.all(far <= rc_cluster * (1 + 1e-6) + 1e-9), (far.max(), rc_cluster)
+    centroid = centres.mean(axis=0)
+    rc_centroid = (np.linalg.norm(centres - centroid, axis=1) + radii).max()
+    return rc_cluster, rc_centroid
+
+
+def test_csg8_cluster_sphere():
+    f = scenes.config("C4", 64, 64)
+    rc_cluster, rc_centroid = check_containment(f.scene)
+    assert abs(rc_centroid - 1.2219) < 2e-3       # the centroid sphere round 1 used
+    assert rc_cluster < 1.04                        # the minimax sphere: 1.033
+    _, _, _, first = bounds_of(f.scene)
+    assert first == 1                               # the plane heads the list, the rest is culled
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_scenes_contained_and_tighter(seed):
+    rng = np.random.default_rng(seed)
+    scene = random_scene(rng, int(rng.integers(2, abi.SDF_MAX_PRIMS + 1)))
+    res = check_containment(scene)
+    if res is not None:
+        rc_cluster, rc_centroid = res
+        # rc_cluster carries the bound's rounding margins (~1e-6 relative
+        # and absolute, twice) and the fp32 rounding of the centre
+        assert rc_cluster <= rc_centroid * (1 + 1e-5) + 1e-5
+
+
+def test_bounds_cache_follows_the_scene():
+    """The cluster search is cached per primitive list: alternating scenes
+    must each get their own answer."""
+    rng = np.random.default_rng(99)
+    a, b = random_scene(rng, 6), random_scene(rng, 7)
+    ra, rb = bounds_of(a), bounds_of(b)
+    for _ in range(3):
+        for s, ref in ((a, ra), (b, rb), (a, ra)):
+            got = bounds_of(s)
+            assert got[0] == ref[0] and got[3] == ref[3]
+            assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2])
+
+
+def test_bounds_refusals():
+    f = scenes.config("C5", 64, 64)
+    rc, *_ = bounds_of(f.scene)
+    assert rc == abi.SDF_E_UNSUPPORTED
+    g = scenes.config("C4", 64, 64)
+    g.scene.prims[3].p[0] = float("nan")
+    rc, *_ = bounds_of(g.scene)
+    assert rc == abi.SDF_E_INVALID_ARG
