@@ -236,7 +236,17 @@ void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
     switch (pr.kind) {
       case SDF_PRIM_SPHERE: R = q[3]; break;
       case SDF_PRIM_BOX: R = std::sqrt(double(q[3]) * q[3] + double(q[4]) * q[4] + double(q[5]) * q[5]); break;
-      case SDF_PRIM_ROUND_BOX: R = std::sqrt(double(q[3]) * q[3] + double(q[4]) * q[4] + double(q[5]) * q[5]); break;
+      case SDF_PRIM_ROUND_BOX: {
+        // the box (b - r) rounded by r (render_kernel.inc sd_round_box; a
+        // negative b - r only shrinks the shape: box_core falls with e)
+        double e2 = 0;
+        for (int j = 3; j < 6; ++j) {
+          const double e = std::max(double(q[j]) - q[6], 0.0);
+          e2 += e * e;
+        }
+        R = std::sqrt(e2) + std::fabs(double(q[6]));
+        break;
+      }
       case SDF_PRIM_TORUS: R = double(q[3]) + q[4]; break;
       case SDF_PRIM_CAPSULE: {
         for (int j = 0; j < 3; ++j) c[j] = 0.5 * (double(q[j]) + q[3 + j]);

@@ -33,8 +33,10 @@ def sphere_of(pr):
     c = p[0:3].copy()
     if pr.kind == abi.PRIM_SPHERE:
         r = p[3]
-    elif pr.kind in (abi.PRIM_BOX, abi.PRIM_ROUND_BOX):
+    elif pr.kind == abi.PRIM_BOX:
         r = np.linalg.norm(p[3:6])
+    elif pr.kind == abi.PRIM_ROUND_BOX:       # the box b - r rounded by r
+        r = np.linalg.norm(np.maximum(p[3:6] - p[6], 0.0)) + abs(p[6])
     elif pr.kind == abi.PRIM_TORUS:
         r = p[3] + p[4]
     elif pr.kind == abi.PRIM_CAPSULE:
@@ -106,7 +108,8 @@ def check_containment(scene):
 def test_csg8_cluster_sphere():
     f = scenes.config("C4", 64, 64)
     rc_cluster, rc_centroid = check_containment(f.scene)
-    assert abs(rc_centroid - 1.2219) < 2e-3       # the centroid sphere round 1 used
+    assert abs(rc_centroid - 1.2088) < 2e-3       # the centroid sphere round 1 used (1.2219 with
+                                                    # its looser round-box sphere)
     assert rc_cluster < 1.04                        # the minimax sphere: 1.033
     _, _, _, first = bounds_of(f.scene)
     assert first == 1                               # the plane heads the list, the rest is culled
