@@ -101,6 +101,9 @@ def parse():
                     help="frame loop: native = sdf_driver_* (C++, RCCL called directly); "
                          "python = multigpu.FrameDriver over torch.distributed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="N=1 fast precision: skip the `exact` sub-object (the same frames "
+                         "in exact precision, bit-exact with the oracle at 4K)")
     ap.add_argument("--clock-warm-s", type=float, default=0.3,
                     help="seconds of render launches before anything is measured (the "
                          "GPU's clocks ramp up over ~0.1 s of load)")
@@ -141,12 +144,22 @@ def rank_flops(frame, tiling, pose):
 
 def pmc_summary(cfg, precision):
     """The committed rocprofv3 PMC summary of the render kernel
-    (profiles/pmc_<cfg>_<precision>.json, written by tools/pmc_traffic.py), or {}."""
+    (profiles/pmc_<cfg>_<precision>.json, written by tools/pmc_traffic.py), or
+    {} -- or {"stale": reason} when it was taken from another build of the
+    kernel than the loaded library's (sdf_kernel_id)."""
+    from sdf3d_amd import abi
     p = ROOT / "profiles" / f"pmc_{cfg}_{precision}.json"
     try:
-        return json.loads(p.read_text())
+        pmc = json.loads(p.read_text())
     except Exception:
         return {}
+    prec = abi.PRECISION_FAST if precision == "fast" else abi.PRECISION_EXACT
+    kid = abi.load_library().sdf_kernel_id(prec)
+    kid = kid.decode() if kid else None
+    if pmc.get("kernel_id") != kid:
+        return {"stale": f"{p.name} was taken from kernel build {pmc.get('kernel_id')}, "
+                         f"the library's is {kid}"}
+    return pmc
 
 
 def valu_cycles_per_unit():
@@ -164,9 +177,12 @@ def roofline(pmc, alg_flops, kavg_ms, store_bytes):
     """The render kernel against the FP32 VALU roofline.
 
     achieved = EXECUTED FP32 flops per launch -- the hardware count
-    64 * (ADD + MUL + TRANS + 2 FMA) wave-instructions from the committed
-    rocprofv3 PMC summary of the same kernel (profiles/pmc_<cfg>_<prec>.json,
-    tools/pmc_traffic.py) -- over the live kernel time; frac <= 1 by
+    64 * (ADD + MUL + TRANS + 2 FMA) wave-instructions weighted by the VALU
+    lane utilisation (SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU): the
+    lanes EXEC left on) from the committed rocprofv3 PMC summary of the same
+    kernel build (profiles/pmc_<cfg>_<prec>.json, tools/pmc_traffic.py,
+    matched by sdf_kernel_id; a summary of another build gives frac null
+    with the reason) -- over the live kernel time; frac <= 1 by
     construction.  valu_busy is the counter-based issue utilisation of the
     same PMC run (SQ_ACTIVE_INST_VALU x the calibrated gfx950 cycles per
     unit / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)); the counter counts a
@@ -177,13 +193,16 @@ def roofline(pmc, alg_flops, kavg_ms, store_bytes):
     roof = {"bound": "valu", "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": None, "traffic": pmc.get("hbm_bytes_per_launch"),
             "kernel_ms": round(kavg_ms, 4),
-            "store_GBps": round(store_bytes / (kavg_ms * 1e-3) / 1e9, 1)}
+            "store_GBps": round(store_bytes / (kavg_ms * 1e-3) / 1e9, 1),
+            "kernel_id": pmc.get("kernel_id")}
+    if "stale" in pmc:
+        roof["frac_null_reason"] = pmc["stale"]
     ex = pmc.get("executed_flops_per_launch")
     if ex:
         ach = ex / (kavg_ms * 1e-3) / 1e12
         roof.update(achieved=round(ach, 2), frac=round(ach / FP32_PEAK_TFLOPS, 4),
-                    executed_flops_per_launch=ex,
-                    basis="executed FP32 flops (PMC) / live kernel time")
+                    executed_flops_per_launch=ex, valu_lane_util=pmc.get("valu_lane_util"),
+                    basis="executed FP32 flops of the active lanes (PMC) / live kernel time")
     c = pmc.get("counters", {})
     cpu = valu_cycles_per_unit()
     if cpu and c.get("SQ_ACTIVE_INST_VALU") and c.get("GRBM_GUI_ACTIVE"):
@@ -433,15 +452,18 @@ def main():
     # rows as RGBA32F, launches serialised on one stream with events around
     # each (in the pipelined frame loop a launch's events would also span
     # time queued behind the other streams' kernels)
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    warm_clocks()
-    for a, b in kev:
-        a.record(ks)
-        rd.render(fk, t, out=kbuf, stream=ks)
-        b.record(ks)
-    torch.cuda.synchronize(dev)
-    kavg_ms = sum(a.elapsed_time(b) for a, b in kev) / len(kev)
+    def kernel_avg_ms(fr):
+        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        warm_clocks()
+        for a, b in kev:
+            a.record(ks)
+            rd.render(fr, t, out=kbuf, stream=ks)
+            b.record(ks)
+        torch.cuda.synchronize(dev)
+        return sum(a.elapsed_time(b) for a, b in kev) / len(kev)
+
+    kavg_ms = kernel_avg_ms(fk)
     log(f"[bench] rank {rank}/{world} {args.config} {W}x{H} rows={rows} "
         f"precision={args.precision} warmup={args.warmup} steps={args.steps}")
     elapsed, kernel_ms, drv = timed_run(frame, args.steps, args.warmup)
@@ -458,6 +480,26 @@ def main():
                    "fps": round(args.steps / el8, 2),
                    "ms_per_step": round(el8 / args.steps * 1e3, 4),
                    "render_ms_pipelined": round(sum(km8) / len(km8), 4) if km8 else None}
+
+    # the same workload in EXACT precision (IEEE div/sqrt, no contraction: the
+    # oracle's fp32 operation sequence, bit-exact with it on every pixel of
+    # the 4K frame, tests/test_gpu_parity.py test_full_size_pixel_parity),
+    # through the same frame driver, with its own kernel time and roofline
+    exact = None
+    if world == 1 and prec == abi.PRECISION_FAST and not args.no_exact:
+        fe = frame.copy()
+        fe.params.precision = abi.PRECISION_EXACT
+        el_e, _, _ = timed_run(fe, args.steps, args.warmup)
+        fek = fe.copy()
+        fek.params.output_format = abi.FORMAT_RGBA32F
+        kavg_e = kernel_avg_ms(fek)
+        pmc_e = pmc_summary(args.config, "exact") if args.format == "rgba32f" else {}
+        exact = {"precision": "exact", "value": round(W * H * args.steps / el_e / 1e6, 3),
+                 "unit": "Mpixels/s", "fps": round(args.steps / el_e, 2),
+                 "ms_per_step": round(el_e / args.steps * 1e3, 4),
+                 "kernel_ms": round(kavg_e, 4),
+                 "roofline": roofline(pmc_e, rank_flops(fe, t, args.pose), kavg_e,
+                                      rows * W * lib_bpp(frame))}
 
     # the same frames without the gather (scaling with and
     # without it): each rank renders its blocks only, max over ranks
@@ -531,6 +573,7 @@ def main():
             "fps": round(args.steps / elapsed, 2),
             "frame_verified": verified,
             "display_rgba8": display,
+            "exact": exact,
             "no_gather": no_gather,
             "kernel_ms": round(kavg_ms, 4),
             # host (CPU) time of the frame loop's own calls per frame, waits

@@ -385,6 +385,15 @@ int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_
  * SDF_DISPATCH_AUTO). */
 int sdf_jit_count(void);
 
+/* Build identity of the built-in render kernels of `precision`
+ * (SDF_PRECISION_*): 16 hex digits of a SHA-256 over the kernel's sources
+ * (its translation unit, render_kernel.inc, kernel_args.h, wave_bits.h,
+ * sdf_abi.h), its compile flags and the compiler's version, fixed when the
+ * library is built.  Measurement tools store it beside counters taken from
+ * the kernel, so a counter summary is never applied to another build.
+ * NULL for an unknown precision. */
+const char* sdf_kernel_id(int32_t precision);
+
 /* The culling bounds a primitive scene's fixed-scene kernels read (host
  * only, no device needed; diagnostics and tests): per primitive
  * bounds[4 * i ..] = {centre.xyz, K_i = (k_i + R_i + 1e-4) / (1 - 1e-5)}

@@ -51,6 +51,9 @@ def load(variant: str = "ieee") -> C.CDLL:
     for fn in (lib.sdf_oracle_render, lib.sdf_oracle_render_f64):
         fn.argtypes = frame_args + [P(abi.sdf_tiling), C.c_void_p, C.c_void_p, C.c_int]
         fn.restype = C.c_int
+    lib.sdf_oracle_replay.argtypes = frame_args + [P(abi.sdf_tiling), C.c_void_p, C.c_void_p,
+                                                   C.c_void_p, C.c_int]
+    lib.sdf_oracle_replay.restype = C.c_int
     lib.sdf_oracle_owned_rows.argtypes = [C.c_int, P(abi.sdf_tiling)]
     lib.sdf_oracle_owned_rows.restype = C.c_int
     lib.sdf_oracle_scene_sdf.argtypes = [P(abi.sdf_scene), C.c_float, C.c_float, C.c_float]
@@ -144,6 +147,35 @@ def render(frame, t=None, nthreads: int | None = None, twin: bool = False,
     if rc != 0:
         raise RuntimeError(f"oracle render failed: {rc}")
     return rgba, steps
+
+
+def replay(frame, steps, t=None, mask=None, nthreads: int | None = None, variant: str = "ieee"):
+    """Forced-step REPLAY (diagnosis only): the fp32 restatement of `frame`
+    with each pixel's primary and shadow marches run for exactly the
+    iterations in `steps` ([rows, W, 2], e.g. a kernel's recorded counts;
+    capped at max_steps) instead of the shader's break tests
+    (voxel_fragment.frag:97-99, :126).  Only pixels where `mask` is true are
+    evaluated (all if None); the others are NaN with steps -1.
+
+    Returns (rgba float32 [rows, W, 4], steps int32 [rows, W, 2])."""
+    lib = load(variant)
+    p = frame.params
+    rows = owned_rows(p.height, t)
+    force = np.ascontiguousarray(np.asarray(steps, dtype=np.int32).reshape(rows, p.width, 2))
+    if mask is not None:
+        force = force.copy()
+        force[~np.asarray(mask, dtype=bool).reshape(rows, p.width), 0] = -2
+    rgba = np.full((rows, p.width, 4), np.nan, dtype=np.float32)
+    out_steps = np.full((rows, p.width, 2), -1, dtype=np.int32)
+    rc = lib.sdf_oracle_replay(C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
+                               C.byref(frame.material), C.byref(frame.params),
+                               C.byref(t) if t is not None else None,
+                               force.ctypes.data_as(C.c_void_p), rgba.ctypes.data_as(C.c_void_p),
+                               out_steps.ctypes.data_as(C.c_void_p),
+                               nthreads if nthreads is not None else default_threads())
+    if rc != 0:
+        raise RuntimeError(f"oracle replay failed: {rc}")
+    return rgba, out_steps
 
 
 def scene_sdf(scene, x: float, y: float, z: float) -> float:

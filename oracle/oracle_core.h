@@ -198,33 +198,45 @@ static REAL FN(scene_sdf)(const sdf_scene* s, FN(v3) p) {
   return d;
 }
 
+/* Forced-step REPLAY (diagnosis only, tests/parity.py): force >= 0 imposes
+ * the march's break point -- exactly min(force, max_steps) iterations, the
+ * break test ignored -- so the oracle can be evaluated at the step counts a
+ * kernel recorded; force < 0 is the shader's own loop. */
+static inline int FN(march_limit)(int max_steps, int force) {
+  return (force >= 0 && force < max_steps) ? force : max_steps;
+}
+
 /* raymarch, voxel_fragment.frag:86-103.  The break test comes after the
  * increment (:97-99); there is no miss branch. */
-static REAL FN(raymarch)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
-                         FN(v3) dir, int32_t* steps) {
+static REAL FN(raymarch_n)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
+                           FN(v3) dir, int force, int32_t* steps) {
   REAL distance = 0;
   REAL max_dist = pa->max_dist, eps = pa->eps;
-  int i;
-  for (i = 0; i < pa->max_steps; i++) {
+  int i, n = FN(march_limit)(pa->max_steps, force);
+  for (i = 0; i < n; i++) {
     FN(v3) ray = FN(add)(pos, FN(muls)(dir, distance));
     REAL sdf = FN(scene_sdf)(s, ray);
     distance += sdf;
-    if (distance > max_dist || sdf < eps) { i++; break; }
+    if (force < 0 && (distance > max_dist || sdf < eps)) { i++; break; }
   }
   *steps = i;
   return distance;
 }
+static REAL FN(raymarch)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
+                         FN(v3) dir, int32_t* steps) {
+  return FN(raymarch_n)(s, pa, pos, dir, -1, steps);
+}
 
 /* shadow, voxel_fragment.frag:105-132 ("improved" soft shadow).  At i == 0
  * the candidate is k*h/max(0, 0) = +inf. */
-static REAL FN(shadow)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
-                       FN(v3) dir, REAL k, int32_t* steps) {
+static REAL FN(shadow_n)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
+                         FN(v3) dir, REAL k, int force, int32_t* steps) {
   REAL distance = 0;
   REAL sdf = (REAL)INFINITY;
   REAL shadow = 1;
   REAL max_dist = pa->max_dist, eps = pa->eps;
-  int i;
-  for (i = 0; i < pa->max_steps; i++) {
+  int i, n = FN(march_limit)(pa->max_steps, force);
+  for (i = 0; i < n; i++) {
     FN(v3) ray = FN(add)(pos, FN(muls)(dir, distance));
     REAL sdf_new = FN(scene_sdf)(s, ray);
     REAL intersection = (i == 0) ? (REAL)0 : sdf_new * sdf_new / ((REAL)2 * sdf);
@@ -232,10 +244,14 @@ static REAL FN(shadow)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
     shadow = FN(gmin)(shadow, k * d_est / FN(gmax)(0, distance - intersection));
     sdf = sdf_new;
     distance += sdf_new;
-    if (distance > max_dist || shadow < eps) { i++; break; }
+    if (force < 0 && (distance > max_dist || shadow < eps)) { i++; break; }
   }
   *steps = i;
   return FN(gclamp)(shadow, 0, 1);
+}
+static REAL FN(shadow)(const sdf_scene* s, const sdf_params* pa, FN(v3) pos,
+                       FN(v3) dir, REAL k, int32_t* steps) {
+  return FN(shadow_n)(s, pa, pos, dir, k, -1, steps);
 }
 
 /* normal, voxel_fragment.frag:134-155: 6-tap central differences. */
@@ -282,12 +298,15 @@ static REAL FN(ambient_occlusion)(const sdf_scene* s, const sdf_params* pa,
 }
 
 /* Fragment stage main(), voxel_fragment.frag:160-211, for one pixel.
- * cam / ray come from the caller (uniform work hoisted, :180, :191-192). */
+ * cam / ray come from the caller (uniform work hoisted, :180, :191-192).
+ * `force` (replay only): NULL, or the (primary, shadow) break points to
+ * impose (march_limit). */
 static void FN(shade_pixel)(const sdf_scene* s, const sdf_light* li,
                             const sdf_material* M, const sdf_params* pa,
-                            FN(v3) cam, FN(v3) ray, float* out, int32_t* st) {
+                            FN(v3) cam, FN(v3) ray, float* out, int32_t* st,
+                            const int32_t* force) {
   int32_t sp = 0, ss = 0;
-  REAL d = FN(raymarch)(s, pa, cam, ray, &sp);                     /* :195 */
+  REAL d = FN(raymarch_n)(s, pa, cam, ray, force ? force[0] : -1, &sp); /* :195 */
   FN(v3) P = FN(add)(cam, FN(muls)(ray, d));                       /* :196 */
   FN(v3) N = pa->normal_mode == SDF_NORMAL_TETRA                   /* :197 */
                  ? FN(normal_tetra)(s, P, pa->normal_eps)
@@ -301,7 +320,7 @@ static void FN(shade_pixel)(const sdf_scene* s, const sdf_light* li,
   if (pa->flags & SDF_FLAG_SHADOW) {                               /* :205 */
     REAL off = pa->shadow_offset, eps = pa->eps;
     FN(v3) o = FN(mk)(P.x + N.x * off * eps, P.y + N.y * off * eps, P.z + N.z * off * eps);
-    sh = FN(shadow)(s, pa, o, incident, (REAL)pa->shadow_k, &ss);
+    sh = FN(shadow_n)(s, pa, o, incident, (REAL)pa->shadow_k, force ? force[1] : -1, &ss);
   }
   REAL dif = FN(gclamp)(FN(dot)(N, incident), 0, 1) * sh;         /* :205 */
   REAL la = li->ambient;
@@ -316,11 +335,16 @@ static void FN(shade_pixel)(const sdf_scene* s, const sdf_light* li,
   if (st) { st[0] = sp; st[1] = ss; }
 }
 
-/* Render the rows owned by `t` (packed order) on the host. */
+/* Render the rows owned by `t` (packed order) on the host.  `force`
+ * (replay only; NULL otherwise): per-pixel (primary, shadow) break points,
+ * laid out like `steps`; a pixel whose primary entry is -2 is skipped (its
+ * outputs are left untouched), so a replay can visit only the pixels a test
+ * needs. */
 static void FN(render_rows)(const sdf_scene* s, const sdf_light* li,
                             const sdf_material* M, const sdf_params* pa,
                             const oracle_uniforms* u, const sdf_tiling* t,
-                            int rows, float* rgba, int32_t* steps, int nthreads) {
+                            int rows, float* rgba, int32_t* steps,
+                            const int32_t* force, int nthreads) {
   int W = pa->width, H = pa->height;
   (void)nthreads;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) if (nthreads > 1)
@@ -336,6 +360,8 @@ static void FN(render_rows)(const sdf_scene* s, const sdf_light* li,
     /* quad.y = (2y+1)/H - 1 (voxel_geometry.geom:26-52 + GL raster). */
     float qy = (float)(2 * y + 1) / (float)H - 1.0f;
     for (int x = 0; x < W; x++) {
+      const int32_t* fo = force ? force + 2 * ((size_t)pr * W + x) : 0;
+      if (fo && fo[0] == -2) continue;
       float qx = (float)(2 * x + 1) / (float)W - 1.0f;
       /* :191 ray = normalize(vec3(quad.x*AR, quad.y, focal)) */
       FN(v3) r0 = FN(normalize)(FN(mk)((REAL)qx * (REAL)u->aspect, qy, u->focal));
@@ -347,7 +373,7 @@ static void FN(render_rows)(const sdf_scene* s, const sdf_light* li,
       FN(v3) ray = FN(normalize)(r1);
       FN(v3) cam = FN(mk)(u->cam[0], u->cam[1], u->cam[2]);
       size_t o = (size_t)pr * W + x;
-      FN(shade_pixel)(s, li, M, pa, cam, ray, rgba + 4 * o, steps ? steps + 2 * o : 0);
+      FN(shade_pixel)(s, li, M, pa, cam, ray, rgba + 4 * o, steps ? steps + 2 * o : 0, fo);
     }
   }
 }

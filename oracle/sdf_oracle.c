@@ -13,6 +13,9 @@
  *                         sdf_defaults, which the tests compare against it)
  *   sdf_oracle_render     fp32 restatement (OpenMP over rows if nthreads > 1)
  *   sdf_oracle_render_f64 fp64 twin (diagnosis of branch flips only)
+ *   sdf_oracle_replay     fp32 restatement with per-pixel break points imposed
+ *                         (forced-step replay: is a kernel's outlier explained
+ *                         by the step counts it recorded?  tests/parity.py)
  */
 #include <math.h>
 #include <stddef.h>
@@ -204,7 +207,7 @@ int sdf_oracle_defaults(sdf_scene* s, sdf_camera* c, sdf_light* l, sdf_material*
 
 static int render(int twin, const sdf_scene* s, const sdf_camera* c, const sdf_light* l,
                   const sdf_material* m, const sdf_params* p, const sdf_tiling* tiling,
-                  float* rgba, int* steps, int nthreads) {
+                  float* rgba, int* steps, const int* force, int nthreads) {
   if (!s || !c || !l || !m || !p || !rgba) return SDF_E_INVALID_ARG;
   if (p->width <= 0 || p->height <= 0) return SDF_E_INVALID_ARG;
   sdf_tiling whole = {8, 0, 1, 0, 1, 1};
@@ -216,22 +219,33 @@ static int render(int twin, const sdf_scene* s, const sdf_camera* c, const sdf_l
   if (rc) return rc;
   if (nthreads < 1) nthreads = 1;
   if (twin)
-    f64_render_rows(s, l, m, p, &u, t, rows, rgba, steps, nthreads);
+    f64_render_rows(s, l, m, p, &u, t, rows, rgba, steps, force, nthreads);
   else
-    f32_render_rows(s, l, m, p, &u, t, rows, rgba, steps, nthreads);
+    f32_render_rows(s, l, m, p, &u, t, rows, rgba, steps, force, nthreads);
   return SDF_OK;
 }
 
 int sdf_oracle_render(const sdf_scene* s, const sdf_camera* c, const sdf_light* l,
                       const sdf_material* m, const sdf_params* p, const sdf_tiling* t,
                       float* rgba, int* steps, int nthreads) {
-  return render(0, s, c, l, m, p, t, rgba, steps, nthreads);
+  return render(0, s, c, l, m, p, t, rgba, steps, 0, nthreads);
 }
 
 int sdf_oracle_render_f64(const sdf_scene* s, const sdf_camera* c, const sdf_light* l,
                           const sdf_material* m, const sdf_params* p, const sdf_tiling* t,
                           float* rgba, int* steps, int nthreads) {
-  return render(1, s, c, l, m, p, t, rgba, steps, nthreads);
+  return render(1, s, c, l, m, p, t, rgba, steps, 0, nthreads);
+}
+
+/* Forced-step replay: the fp32 restatement with each pixel's primary and
+ * shadow marches run for exactly force[2i], force[2i+1] iterations (capped
+ * at max_steps; oracle_core.h march_limit); pixels with force[2i] == -2 are
+ * skipped and their rgba / steps left as the caller filled them. */
+int sdf_oracle_replay(const sdf_scene* s, const sdf_camera* c, const sdf_light* l,
+                      const sdf_material* m, const sdf_params* p, const sdf_tiling* t,
+                      const int* force, float* rgba, int* steps, int nthreads) {
+  if (!force) return SDF_E_INVALID_ARG;
+  return render(0, s, c, l, m, p, t, rgba, steps, force, nthreads);
 }
 
 /* Scene-SDF probe for known-answer tests: d = sceneSDF(p) in fp32. */

@@ -122,6 +122,7 @@ SIGNATURES = {
     "sdf_format_bytes": (C.c_int, [C.c_int32]),
     "sdf_tiles_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
     "sdf_jit_count": (C.c_int, []),
+    "sdf_kernel_id": (C.c_char_p, [C.c_int32]),
     "sdf_scene_bounds": (C.c_int, [_P(sdf_scene), _P(C.c_float), _P(C.c_float), _P(C.c_int32)]),
     "sdf_tiles_decode": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
                                    C.c_int32, C.c_void_p, C.c_void_p]),

@@ -628,6 +628,15 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera, const sdf_light
 
 int sdf_jit_count(void) { return sdf::jit_compiled_count(); }
 
+// SDF_KERNEL_ID_EXACT / _FAST: written by sdf3d_amd/build.py (kernel_id())
+#include "kernel_id.inc"
+
+const char* sdf_kernel_id(int32_t precision) {
+  if (precision == SDF_PRECISION_EXACT) return SDF_KERNEL_ID_EXACT;
+  if (precision == SDF_PRECISION_FAST) return SDF_KERNEL_ID_FAST;
+  return nullptr;
+}
+
 int sdf_scene_bounds(const sdf_scene* scene, float* bounds, float* cluster,
                      int32_t* cluster_first) {
   if (!scene || !bounds || !cluster || !cluster_first) return SDF_E_INVALID_ARG;

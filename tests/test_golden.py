@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle
-from parity import assert_parity, report
+from parity import assert_parity, compare
 from golden.make_golden import FIXTURES, frame_for
 
 GOLD = Path(__file__).resolve().parent / "golden"
@@ -37,7 +37,9 @@ def test_fixture_integrity_and_oracle_reproduces(name):
 def test_fp64_twin_agrees(name):
     rgba, steps = load_fixture(name)
     t64, s64 = oracle.render(frame_for(name), twin=True)
-    rep = report(t64, s64, rgba, steps)
+    # outliers must be explained by the fp32 oracle stopped at the twin's
+    # own step counts (forced-step replay, parity.py)
+    rep = compare(frame_for(name), t64, s64, rgba, steps)
     assert_parity(rep, what=name)
 
 

@@ -184,7 +184,7 @@ def test_cpp_driver_multirank_arcball(tmp_path, world):
     import numpy as np
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle
-    from parity import assert_parity, quantize, report
+    from parity import assert_parity, compare, quantize
     from sdf3d_amd import Renderer, abi, scenes
     from test_camera import nav_views
     exe = ROOT / "sdf3d_amd" / "bin" / "sdf_main"
@@ -214,4 +214,4 @@ def test_cpp_driver_multirank_arcball(tmp_path, world):
     want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
     assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
     ref, rst = oracle.render(f)
-    assert_parity(report(rgba, st, ref, rst, oracle.render(f, twin=True)[0]), what="arcball")
+    assert_parity(compare(f, rgba, st, ref, rst), what="arcball")

@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from parity import assert_parity, report
+from parity import assert_parity, compare
 from sdf3d_amd import abi, scenes
 
 pytestmark = pytest.mark.gpu
@@ -68,7 +68,7 @@ def test_jit_kernel_matches_unculled(renderer, seed):
             assert np.array_equal(sa, sb)
             assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
         else:
-            assert_parity(report(a, sa, b, sb), what=f"jit seed {seed}")
+            assert_parity(compare(f, a, sa, b, sb, ref_is_oracle=False), what=f"jit seed {seed}")
     # a new signature compiles once per precision; the second frame reuses it
     assert jit_count(renderer) - before in (0, 1, 2)
     n = jit_count(renderer)

@@ -19,8 +19,8 @@ import pytest
 
 import oracle
 from golden.make_golden import FIXTURES, frame_for
-from parity import (assert_parity, assert_parity_frame, quantize, reading_spread,
-                    report)
+from parity import (assert_parity, assert_parity_frame, compare, full_size_conditioning,
+                    quantize, reading_spread, report)
 from sdf3d_amd import abi, renderer as R, scenes
 
 pytestmark = pytest.mark.gpu
@@ -55,30 +55,37 @@ def log(key, rep):
     print(key, json.dumps(rep))
 
 
-def check_frame(key, frame, rgba, steps, ref, ref_steps, t=None, readings=None):
-    """Parity of one GPU frame against the oracle.  Exact precision: the
-    strict policy.  Fast precision: the strict policy unless the frame is
-    fp32-ill-conditioned (the fp64 twin or the contracted fp32 reading fails
-    it against the oracle, or the scene is the Mandelbulb, where they fail it
-    at 320x180 and 4K), then the readings' spread (parity.py)."""
-    if readings is None:
-        readings = {"twin": oracle.render(frame, t, twin=True),
-                    "fma": oracle.render(frame, t, variant="fma")}
-    rep = report(rgba, steps, ref, ref_steps, readings["twin"][0],
-                 alt_rgba=[readings["fma"][0]])
+def check_frame(key, frame, rgba, steps, ref, ref_steps, t=None):
+    """Parity of one GPU frame against the oracle, outliers diagnosed by the
+    forced-step replay at the kernel's recorded step counts (parity.py).
+    Exact precision: the strict policy.  Fast precision: the strict policy
+    unless this frame is measured fp32-ill-conditioned (the fp64 twin or the
+    contracted fp32 reading fails it against the oracle under the same
+    replay diagnosis) or at the BASELINE size of its scene and pose
+    (tests/golden/conditioning.json), then the readings' spread with its
+    magnitude bound."""
     if frame.params.precision == abi.PRECISION_EXACT:
+        rep = compare(frame, rgba, steps, ref, ref_steps, t)
         rep["policy"] = "strict"
         log(key, rep)
         assert_parity(rep, what=key)
-    else:
-        spread = reading_spread(ref, ref_steps, readings)
-        rep["readings"] = {n: {k: r[k] for k in ("outliers", "undiagnosed", "over_max_err",
-                                                 "max_err")} for n, r in spread.items()}
-        ill = frame.scene.kind == abi.SCENE_MANDELBULB
-        try:
-            rep["policy"] = assert_parity_frame(rep, spread, what=key, ill_conditioned=ill)
-        finally:
-            log(key, rep)
+        return rep
+    readings = {"twin": oracle.render(frame, t, twin=True),
+                "fma": oracle.render(frame, t, variant="fma")}
+    rep = compare(frame, rgba, steps, ref, ref_steps, t, twin_rgba=readings["twin"][0],
+                  alt_rgba=[readings["fma"][0]])
+    spread = reading_spread(frame, ref, ref_steps, readings, t)
+    rep["readings"] = {n: {k: r[k] for k in ("outliers", "replay_diagnosed", "undiagnosed",
+                                             "undiagnosed_max_err", "over_max_err", "max_err")}
+                       for n, r in spread.items()}
+    full = full_size_conditioning(frame)
+    rep["full_size_conditioning"] = None if full is None else {
+        n: {k: full[n][k] for k in ("outlier_rate", "undiagnosed_rate", "undiagnosed_max_err")}
+        for n in ("twin", "fma")}
+    try:
+        rep["policy"] = assert_parity_frame(rep, spread, what=key, full_size=full)
+    finally:
+        log(key, rep)
     return rep
 
 
@@ -117,7 +124,7 @@ def test_specialised_matches_generic(renderer, cfg, pose):
         if prec == abi.PRECISION_EXACT or cfg == "C5":
             assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(sa, sb)
         else:
-            assert_parity(report(a, sa, b, sb), what=cfg)
+            assert_parity(compare(f, a, sa, b, sb, ref_is_oracle=False), what=cfg)
 
 
 def test_exact_mode_is_mostly_bit_exact(renderer):
@@ -140,7 +147,7 @@ def test_every_csg_op(renderer, op):
         f.scene.prims[i].k = 0.1
     rgba, steps = gpu(renderer, f)
     ref, ref_steps = oracle.render(f)
-    rep = report(rgba, steps, ref, ref_steps, oracle.render(f, twin=True)[0])
+    rep = compare(f, rgba, steps, ref, ref_steps)
     log(f"csg_op/{abi.OP_NAMES[op]}", rep)
     assert_parity(rep, what=abi.OP_NAMES[op])
 
@@ -159,7 +166,7 @@ def test_feature_variants(renderer, mutate, name):
     mutate(f)
     rgba, steps = gpu(renderer, f)
     ref, ref_steps = oracle.render(f)
-    rep = report(rgba, steps, ref, ref_steps, oracle.render(f, twin=True)[0])
+    rep = compare(f, rgba, steps, ref, ref_steps)
     log(f"variant/{name}", rep)
     assert_parity(rep, what=name)
 
@@ -170,7 +177,7 @@ def test_ragged_sizes(renderer, w, h):
         f = scenes.config("C3", w, h, precision=prec, pose=1)
         rgba, steps = gpu(renderer, f)
         ref, ref_steps = oracle.render(f)
-        rep = report(rgba, steps, ref, ref_steps, oracle.render(f, twin=True)[0])
+        rep = compare(f, rgba, steps, ref, ref_steps)
         assert_parity(rep, what=f"{w}x{h}/{prec}")
 
 
@@ -197,7 +204,7 @@ def test_tiling_and_deinterleave_reassemble_frame(renderer, world):
     ref, ref_st = oracle.render(f, t)
     n = R.owned_rows(f.params.height, t)
     assert np.array_equal(part, parts[(world - 1) * stride:(world - 1) * stride + n].cpu().numpy())
-    assert_parity(report(part, pst, ref, ref_st, oracle.render(f, t, twin=True)[0]), what="part")
+    assert_parity(compare(f, part, pst, ref, ref_st, t), what="part")
 
 
 @pytest.mark.parametrize("world,shares", [(3, (1, 2)), (8, (1, 3))])
@@ -223,8 +230,7 @@ def test_weighted_tiling_renders_its_rows(renderer, world, shares):
     t = R.tiling(1, world, 8, shares=shares)
     part, pst = gpu(renderer, f, t)
     ref, ref_st = oracle.render(f, t)
-    assert_parity(report(part, pst, ref, ref_st, oracle.render(f, t, twin=True)[0]),
-                  what="weighted part")
+    assert_parity(compare(f, part, pst, ref, ref_st, t), what="weighted part")
 
 
 def test_empty_tiling_is_noop(renderer):
@@ -361,7 +367,7 @@ def test_output_formats(renderer, fmt, prec):
         # a float format: the RGBA32F parity policy applies (alpha is 1)
         rgba = np.concatenate([out, np.ones_like(out[..., :1])], -1)
         _, gst = gpu(renderer, f)
-        assert_parity(report(rgba, gst, orc, ost), what="rgb32f")
+        assert_parity(compare(f, rgba, gst, orc, ost), what="rgb32f")
     else:
         diff = np.abs(out.astype(np.float64) - quantize(orc, fmt).astype(np.float64))
         # one LSB at most; how often a boundary is crossed depends on the float
@@ -569,8 +575,8 @@ def test_culling_exact_on_random_scenes(renderer, seed):
     a, sa = gpu(renderer, f)
     b, sb = gpu(renderer, u)
     c, sc = gpu(renderer, g)
-    assert_parity(report(a, sa, b, sb), what=f"seed {seed}")
-    assert_parity(report(c, sc, b, sb), what=f"seed {seed} generic")
+    assert_parity(compare(f, a, sa, b, sb, ref_is_oracle=False), what=f"seed {seed}")
+    assert_parity(compare(f, c, sc, b, sb, ref_is_oracle=False), what=f"seed {seed} generic")
 
 
 @pytest.mark.parametrize("light,k", [

@@ -14,8 +14,11 @@ bench's path: exact shadow skip active) and with one, and on the CPU:
 It reports the parity policy's numbers for GPU-vs-oracle, and the same
 numbers for twin-vs-oracle and fma-vs-oracle: how far two valid readings of
 the reference already disagree at this size, which bounds what any fp32
-implementation can promise.  Large outliers (> 0.05) are listed with their
-step counts in every reading.
+implementation can promise.  Every outlier is diagnosed by the forced-step
+replay (tests/parity.py: the fp32 oracle stopped at the kernel's or the
+reading's own step counts must reproduce its value within 1e-4).  Large
+outliers (> 0.05) are listed with their step counts in every reading and
+their replay error.
 
     python tools/fullsize_parity.py --out gpurun_out/fullsize_parity.json
 """
@@ -49,7 +52,7 @@ def main():
     import torch
 
     import oracle
-    from parity import report
+    from parity import compare, pixel_err
     from sdf3d_amd import Renderer, abi, scenes
 
     rd = Renderer("cuda:0")
@@ -66,8 +69,8 @@ def main():
         e_twin, e_fma = err_of(twin, ref), err_of(fma, ref)
         spread = {
             "oracle_s": round(t_ref, 2), "twin_s": round(t_twin, 2),
-            "twin_vs_oracle": report(twin, tst, ref, rst),
-            "fma_vs_oracle": report(fma, fst, ref, rst),
+            "twin_vs_oracle": compare(f0, twin, tst, ref, rst),
+            "fma_vs_oracle": compare(f0, fma, fst, ref, rst),
             "twin_over_0.05": int((e_twin > 0.05).sum()),
             "fma_over_0.05": int((e_fma > 0.05).sum()),
         }
@@ -81,22 +84,21 @@ def main():
             torch.cuda.synchronize()
             same = bool(torch.equal(g.view(torch.int32), gs.view(torch.int32)))
             g, st = g.cpu().numpy(), st.cpu().numpy()
-            rep = report(g, st, ref, rst, twin)
+            rep = compare(f, g, st, ref, rst, twin_rgba=twin, alt_rgba=[fma])
             e = err_of(g, ref)
-            fma_dis = err_of(fma, ref) > 1e-4
-            out_mask = e > 1e-4
             diag_steps = np.any(st != rst, axis=-1)
-            rep["undiagnosed_with_fma"] = int(np.sum(out_mask & ~diag_steps
-                                                    & ~(e_twin > 1e-4) & ~fma_dis))
             rep["steps_equal_frac"] = float(np.mean(~diag_steps))
+            rep["outliers_steps_equal"] = int(np.sum((e > 1e-4) & ~diag_steps))
             rep["nostep_equals_steps_render"] = same
             big = np.argwhere(e > 0.05)
-            rep["over_0.05"] = int(len(big))
+            rp, _ = oracle.replay(f, st, mask=e > 0.05)
+            e_rp = pixel_err(g, rp)
             rep["over_0.05_samples"] = [
                 {"y": int(y), "x": int(x), "err": float(e[y, x]), "gpu_steps": st[y, x].tolist(),
                  "oracle_steps": rst[y, x].tolist(), "twin_steps": tst[y, x].tolist(),
                  "fma_steps": fst[y, x].tolist(), "twin_err": float(e_twin[y, x]),
-                 "fma_err": float(e_fma[y, x])} for y, x in big[:12]]
+                 "fma_err": float(e_fma[y, x]), "replay_err": float(e_rp[y, x])}
+                for y, x in big[:12]]
             # of the GPU's outliers above 0.05, how many are pixels where a
             # valid reading also flips (twin or fma steps differ from oracle)
             flips_other = np.any(tst != rst, axis=-1) | np.any(fst != rst, axis=-1)

@@ -15,18 +15,19 @@ STEPS=${STEPS:-pmc configs bench prof trace}
 for s in $STEPS; do
   case $s in
     pmc)
-      for c in C4 C5 C2; do
-        timeout -k 10 400 python tools/pmc_traffic.py --config $c --precision fast \
-          --out gpurun_out/pmc > gpurun_out/pmc_$c.log 2>&1
-        rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
-        cp gpurun_out/pmc/pmc_${c}_fast.json profiles/
+      for spec in ${PMC_SPECS:-C4:fast C4:exact C5:fast C5:exact C2:fast}; do
+        c=${spec%%:*}; p=${spec##*:}
+        timeout -k 10 400 python tools/pmc_traffic.py --config $c --precision $p \
+          --out gpurun_out/pmc > gpurun_out/pmc_${c}_$p.log 2>&1
+        rc=$?; echo "pmc $c $p rc=$rc"; [ $rc -ne 0 ] && exit $rc
+        cp gpurun_out/pmc/pmc_${c}_$p.json profiles/
       done ;;
     configs)
       : > gpurun_out/configs.jsonl
       for spec in "C4 fast" "C4 exact" "C3 fast" "C2 fast" "C5 fast" "C5 exact" "C1 fast"; do
         set -- $spec
         timeout -k 10 300 python bench.py --config $1 --precision $2 --steps 30 --warmup 3 \
-          --no-cpu-baseline --no-display >> gpurun_out/configs.jsonl 2>> gpurun_out/configs.log
+          --no-cpu-baseline --no-display --no-exact >> gpurun_out/configs.jsonl 2>> gpurun_out/configs.log
         rc=$?; echo "$spec rc=$rc"; [ $rc -ne 0 ] && exit $rc
       done ;;
     bench)
@@ -36,12 +37,12 @@ for s in $STEPS; do
       rm -rf gpurun_out/prof
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
         -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-display \
-        --streams 1 > gpurun_out/prof.log 2>&1
+        --no-exact --streams 1 > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     trace)
       rm -rf gpurun_out/trace3
       timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace3 \
-        -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-display \
+        -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-display --no-exact \
         > gpurun_out/trace3.log 2>&1
       rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
       python tools/trace_union.py gpurun_out/trace3 --frames 50 \

@@ -25,7 +25,7 @@ for s in $STEPS; do
     prof)
       rm -rf gpurun_out/prof
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-        python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-display --streams 1 ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
+        python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-display --no-exact --streams 1 ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; find gpurun_out/prof -name '*stats*' | head
       fatal $rc && exit $rc ;;
   esac
