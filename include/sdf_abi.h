@@ -387,7 +387,7 @@ int sdf_jit_count(void);
 
 /* Build identity of the built-in render kernels of `precision`
  * (SDF_PRECISION_*): 16 hex digits of a SHA-256 over the kernel's sources
- * (its translation unit, render_kernel.inc, kernel_args.h, wave_bits.h,
+ * (its translation unit, render_kernel.inc, kernel_args.h, wave_bits.h, cr_math.h,
  * sdf_abi.h), its compile flags and the compiler's version, fixed when the
  * library is built.  Measurement tools store it beside counters taken from
  * the kernel, so a counter summary is never applied to another build.

@@ -1,0 +1,152 @@
+// cr_math.h -- correctly rounded fp32 building blocks for the EXACT-precision
+// kernel (render_exact.hip), cheaper on gfx950 than the compiler's generic
+// sequences yet bit-identical to what the oracle computes (IEEE sqrtf, a / b,
+// and log evaluated in fp64 and rounded once: oracle/sdf_oracle.c cr_logf).
+//
+//   cr_sqrt(x)           == sqrtf(x) for every x.  Fast path on [2^-100,
+//                           2^100): v_rsq, then one Newton/Markstein
+//                           correction (rsq, 2 mul, 2 fma) instead of the
+//                           generic v_sqrt + denormal scaling + 2-candidate
+//                           residual test + class fix-up (17 instructions).
+//   div_prepared(a,b,yb) == a / b, given yb = RN(1/b) prepared on the host,
+//                           by Markstein's theorem (q within 1 ulp, r exact,
+//                           fma(r, yb, q) = RN(a/b)) wherever a/b, q and r
+//                           neither overflow nor underflow (3 instructions
+//                           instead of 11).  div_scaled applies it to the
+//                           smooth-min's h = n / k (render_kernel.inc smin)
+//                           after an exact power-of-two scaling that puts
+//                           every positive k in its domain.
+//   cr_log(x)            == (float)log((double)x) for every x.  Fast path:
+//                           m in [sqrt(1/2), sqrt(2)), f = (m-1)/(m+1) with a
+//                           refined v_rcp_f64, 2 f (1 + s/3 + ... + s^8/17)
+//                           with s = f^2, plus e ln2, in fp64 (error below
+//                           2^-49 relative); when that value lies too close to
+//                           a float rounding boundary to round it safely, or x
+//                           is not a positive normal float, the lane takes the
+//                           fp64 library log the oracle's reading is.
+//
+// Every fast path is taken by a lane only where it is proven or checked
+// bit-identical; the fall-backs run in a branch the wave skips when no lane
+// needs it.  tests/crmath/crmath_check.hip runs these functions EXHAUSTIVELY
+// on the GPU (all 2^32 inputs for cr_sqrt and cr_log; the smooth-min domain
+// for div_prepared) against the generic sequences (tests/test_gpu_crmath.py).
+#pragma once
+
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+
+namespace sdf {
+namespace crm {
+
+// a wave-uniform "does any lane need the slow path" (no divergent branch)
+__device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+// Placed in a slow-path block: an instruction with side effects keeps LLVM
+// from if-converting the block into selects, i.e. from computing the slow
+// path on every lane of every wave.
+#define SDF_CRM_COLD() asm volatile("" ::: "memory")
+
+// x in [2^-100, 2^100) (positive, normal, far from both ends of the range):
+// the fast path's x * y, s * s and residual neither underflow nor overflow
+__device__ __forceinline__ bool sqrt_fast_ok(float x) {
+  return (__float_as_uint(x) - 0x0D800000u) < (0x71800000u - 0x0D800000u);
+}
+
+__device__ __forceinline__ float sqrt_fast(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);   // 1/sqrt(x), ~1 ulp
+  const float s = x * y;                      // sqrt(x), within ~2 ulp
+  const float h = 0.5f * y;                   // 1/(2 sqrt(x)), exact halving
+  const float r = __builtin_fmaf(-s, s, x);   // x - s^2, exact
+  return __builtin_fmaf(h, r, s);
+}
+
+__device__ __forceinline__ float cr_sqrt(float x) {
+  float s = sqrt_fast(x);
+  const bool ok = sqrt_fast_ok(x);
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+    s = ok ? s : __builtin_sqrtf(x);
+  }
+  return s;
+}
+
+// 1/x for x in [2^-100, 2^100) (the caller's domain; no guard): v_rcp and
+// one Newton step with an exact fma residual, checked equal to IEEE 1.0f / x
+// on every float of that range
+__device__ __forceinline__ float rcp_fast(float x) {
+  const float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  return __builtin_fmaf(e, y, y);
+}
+
+// a / b = RN(a/b) from yb = RN(1/b) (Markstein): valid where no intermediate
+// underflows or overflows -- the caller's domain argument.
+__device__ __forceinline__ float div_prepared(float a, float b, float yb) {
+  const float q = a * yb;
+  const float r = __builtin_fmaf(-b, q, a);
+  return __builtin_fmaf(r, yb, q);
+}
+
+// n / k for the smooth-min (n in [0, k], any positive finite k), from the
+// host-prepared sc = 2^s with k sc in [2^-22, 2) (s <= 127) and ys =
+// RN(1/(k sc)): n/k = (n sc)/(k sc) exactly, k sc is exact, n sc is exact
+// unless it underflows (then h < 2^-104), and Markstein's conditions hold
+// for n sc >= 2^-100.  Below that h < 2^-78 on both paths, so h*h -- all the
+// smooth-min uses -- is +0 on both: the smooth-min's result is bit-identical.
+__device__ __forceinline__ float div_scaled(float n, float k, float sc, float ys) {
+  return div_prepared(n * sc, k * sc, ys);
+}
+
+// ---- natural log ----------------------------------------------------------
+// log(2) as a double (the rounding error, 2^-54 relative, times |e| <= 126
+// stays far below the fast path's error bound)
+#define SDF_CRM_LN2 0.693147180559945309417232121458
+// relative error bound of log_fast's double result (analysis: series
+// truncation s^9/19 <= 2^-50 relative at |f| <= 0.1716, the refined
+// reciprocal and the ~20 fp64 roundings each <= 2^-52; a generous 2^-47)
+#define SDF_CRM_LOG_EPS 7.105427357601002e-15
+
+__device__ __forceinline__ double log_fast(float x) {
+  // x = 2^e m, m in [sqrt(1/2), sqrt(2))
+  float mf = __builtin_amdgcn_frexp_mantf(x);            // [0.5, 1)
+  int e = __builtin_amdgcn_frexp_expf(x);
+  if (mf < 0.70710678f) {
+    mf = mf * 2.0f;                                      // exact
+    e = e - 1;
+  }
+  const double m = (double)mf;
+  const double d = m + 1.0;                              // exact
+  double y = __builtin_amdgcn_rcp(d);                    // ~2^-23 relative
+  y = __builtin_fma(__builtin_fma(-d, y, 1.0), y, y);    // ~2^-46
+  y = __builtin_fma(__builtin_fma(-d, y, 1.0), y, y);    // ~2^-52
+  const double f = (m - 1.0) * y;                        // m - 1 exact
+  const double s = f * f;
+  double p = 1.0 / 17.0;
+  p = __builtin_fma(p, s, 1.0 / 15.0);
+  p = __builtin_fma(p, s, 1.0 / 13.0);
+  p = __builtin_fma(p, s, 1.0 / 11.0);
+  p = __builtin_fma(p, s, 1.0 / 9.0);
+  p = __builtin_fma(p, s, 1.0 / 7.0);
+  p = __builtin_fma(p, s, 1.0 / 5.0);
+  p = __builtin_fma(p, s, 1.0 / 3.0);
+  const double lm = 2.0 * f + (2.0 * f) * (s * p);      // 2 atanh(f) = log(m)
+  return __builtin_fma((double)e, SDF_CRM_LN2, lm);
+}
+
+__device__ __forceinline__ float cr_log(float x) {
+  const double v = log_fast(x);
+  // round safely: both ends of v's error interval round to the same float
+  const double tol = SDF_CRM_LOG_EPS * __builtin_fabs(v);
+  const float r = (float)v;
+  const bool ok = ((float)(v - tol) == r) & ((float)(v + tol) == r) &
+                  ((__float_as_uint(x) - 0x00800000u) < (0x7F800000u - 0x00800000u));
+  float out = r;
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+    out = ok ? r : (float)log((double)x);
+  }
+  return out;
+}
+
+}  // namespace crm
+}  // namespace sdf

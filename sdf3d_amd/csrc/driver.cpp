@@ -57,6 +57,9 @@ struct Rccl {
   void* handle = nullptr;
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  // optional: non-blocking creation (sdf_comm_create); without it a helper
+  // thread runs the blocking ncclCommInitRank
+  ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
@@ -96,6 +99,8 @@ Rccl* load_rccl(const char* path) {
   sym(r->Recv, "ncclRecv");
   sym(r->GroupStart, "ncclGroupStart");
   sym(r->GroupEnd, "ncclGroupEnd");
+  r->CommInitRankConfig = reinterpret_cast<decltype(r->CommInitRankConfig)>(
+      dlsym(h, "ncclCommInitRankConfig"));
   if (!ok) {
     delete r;
     dlclose(h);
@@ -156,6 +161,25 @@ namespace {
 
 int hip_ok(hipError_t e) { return e == hipSuccess ? SDF_OK : SDF_E_HIP; }
 int nccl_ok(ncclResult_t e) { return e == ncclSuccess ? SDF_OK : SDF_E_COMM; }
+
+// A communicator created non-blocking (sdf_comm_create) may answer any call
+// with ncclInProgress while RCCL finishes it in the background; the next call
+// on it must wait for the communicator to settle (ncclCommGetAsyncError
+// leaving ncclInProgress), polled here with a limit.
+ncclResult_t settle(const sdf_comm* c, ncclResult_t rc, int timeout_ms) {
+  if (rc != ncclInProgress) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto limit = std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 60000);
+  for (unsigned n = 0;; ++n) {
+    ncclResult_t st = ncclSuccess;
+    if (c->api->CommGetAsyncError(c->comm, &st) != ncclSuccess) return ncclSystemError;
+    if (st != ncclInProgress) return st;
+    if ((n & 63) == 63) {
+      if (std::chrono::steady_clock::now() - t0 > limit) return ncclInProgress;
+      sched_yield();
+    }
+  }
+}
 
 int fail(sdf_driver* d, int rc) {
   if (rc != SDF_OK && d->error == SDF_OK) d->error = rc;
@@ -239,7 +263,9 @@ int ship(sdf_driver* d, long long j) {
       if (d->sends[r])
         rc = nccl_ok(R.Recv(static_cast<char*>(d->gathered[b]) + (size_t)r * d->pitch,
                             (size_t)(d->data_off[r] + sz[r]), ncclUint8, r, comm, d->ds));
-  const int rc_end = nccl_ok(R.GroupEnd());
+  // (a non-blocking communicator may still be enqueueing: settle before the
+  // event below is recorded behind the group's kernels)
+  const int rc_end = nccl_ok(settle(d->data_comm, R.GroupEnd(), d->timeout_ms));
   d->t_group += seconds_since(tg);
   if (rc == SDF_OK) rc = rc_end;
   if (rc != SDF_OK) return fail(d, rc);
@@ -287,11 +313,14 @@ int sdf_comm_unique_id(const char* rccl_path, void* id) {
   return SDF_OK;
 }
 
-// ncclCommInitRank blocks until every rank has joined.  It runs on a helper
-// thread so that the caller gets SDF_E_TIMEOUT after `timeout_ms` when a
-// peer never joins (a peer that failed, or an id from an earlier run): the
-// helper is then left blocked, and the process is expected to report the
-// error and exit.
+// Creation waits until every rank has joined, at most `timeout_ms`: a peer
+// that never joins (it failed, or the id is from an earlier run) gives
+// SDF_E_TIMEOUT.  With ncclCommInitRankConfig the communicator is created
+// non-blocking (config.blocking = 0) and polled with ncclCommGetAsyncError;
+// on the limit it is aborted (ncclCommAbort), so nothing of it is left
+// running in the process.  An RCCL without that entry point gets the blocking
+// ncclCommInitRank on a helper thread, which on a timeout is left blocked
+// (it aborts the communicator if it ever returns).
 int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32_t rank,
                     int32_t timeout_ms, sdf_comm** comm) {
   if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return SDF_E_INVALID_ARG;
@@ -300,6 +329,26 @@ int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32
   if (!R) return SDF_E_COMM;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return SDF_E_NO_DEVICE;
+  if (R->CommInitRankConfig) {
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+    config.blocking = 0;
+    ncclComm_t c = nullptr;
+    ncclResult_t rc = R->CommInitRankConfig(&c, nranks, uid, rank, &config);
+    if (rc != ncclSuccess && rc != ncclInProgress) {
+      if (c) R->CommAbort(c);
+      return SDF_E_COMM;
+    }
+    sdf_comm probe{R, c, nranks, rank, dev};
+    rc = c ? settle(&probe, ncclInProgress, timeout_ms > 0 ? timeout_ms : 120000) : ncclSystemError;
+    if (rc != ncclSuccess) {
+      if (c) R->CommAbort(c);
+      return rc == ncclInProgress ? SDF_E_TIMEOUT : SDF_E_COMM;
+    }
+    *comm = new sdf_comm{R, c, nranks, rank, dev};
+    return SDF_OK;
+  }
   struct Init {
     std::mutex mu;
     std::condition_variable cv;
@@ -544,8 +593,10 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
   rc = hip_ok(hipStreamWaitEvent(d->ss, d->ev_render[b], 0));
   if (rc != SDF_OK) return fail(d, rc);
   int32_t* sz = d->sizes_dev + (size_t)b * d->world;
-  rc = nccl_ok(d->size_comm->api->AllGather(d->sender ? d->local[b] : (void*)d->zero_dev, sz, 1,
-                                            ncclInt32, d->size_comm->comm, d->ss));
+  rc = nccl_ok(settle(d->size_comm,
+                      d->size_comm->api->AllGather(d->sender ? d->local[b] : (void*)d->zero_dev,
+                                                   sz, 1, ncclInt32, d->size_comm->comm, d->ss),
+                      d->timeout_ms));
   if (rc == SDF_OK)
     rc = hip_ok(hipMemcpyAsync(d->sizes_host + (size_t)b * d->world, sz,
                                sizeof(int32_t) * d->world, hipMemcpyDeviceToHost, d->ss));

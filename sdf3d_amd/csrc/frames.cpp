@@ -11,8 +11,11 @@
 // pixels are those of sdf_render bit for bit (same shade_pixel).
 //
 // Work counters: a small per-device pool, zeroed on the caller's stream
-// before each launch.  A slot is reused after kCounterSlots launches, so up
-// to that many launches may be in flight at once on different streams.
+// before each launch.  A slot is reused round-robin after kCounterSlots
+// launches; each slot's last launch records an event that its next user's
+// stream waits for before zeroing it, so any number of launches may be in
+// flight on any streams (a reused slot must not be reset under a
+// kernel still taking tiles from it).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -34,7 +37,10 @@ constexpr int kSlotBytes = kFrameQueues * kQueueStride * 4;   // one launch's qu
 struct DeviceFrames {
   uint8_t* counters = nullptr;
   int blocks = 0;                    // persistent grid: 8 waves x 4 SIMDs per CU / 4 waves
-  std::atomic<unsigned> next{0};
+  std::mutex mu;                     // slot choice + its event wait/record, per device
+  unsigned next = 0;
+  hipEvent_t done[kCounterSlots] = {};   // the slot's last launch (recorded after it)
+  bool used[kCounterSlots] = {};
 };
 
 std::mutex g_mu;
@@ -53,6 +59,8 @@ DeviceFrames* device_state(int dev) {
     auto* d = new DeviceFrames;
     d->counters = static_cast<uint8_t*>(p);
     d->blocks = cus * 8;   // 256-thread groups: 4 waves each, 32 waves per CU
+    for (hipEvent_t& e : d->done)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     g_dev[dev] = d;
   }
   return g_dev[dev];
@@ -130,8 +138,13 @@ extern "C" int sdf_render_frames(const sdf_scene* scene, const sdf_camera* camer
       fc.steps = steps ? steps[f0 + j] : nullptr;
     }
     fa.nframes = nf;
-    const unsigned slot = ds->next.fetch_add(1) % sdf::kCounterSlots;
+    std::lock_guard<std::mutex> lock(ds->mu);
+    const unsigned slot = ds->next++ % sdf::kCounterSlots;
     fa.counter = reinterpret_cast<uint32_t*>(ds->counters + slot * sdf::kSlotBytes);
+    // the slot's previous launch (on whatever stream) ends before it is reset
+    if (ds->used[slot] &&
+        hipStreamWaitEvent((hipStream_t)stream, ds->done[slot], 0) != hipSuccess)
+      return SDF_E_HIP;
     // no more groups than tiles need (4 waves per group)
     const long long items = (long long)nf * fa.tiles_per_frame;
     const long long want = (items + 3) / 4;
@@ -146,6 +159,8 @@ extern "C" int sdf_render_frames(const sdf_scene* scene, const sdf_camera* camer
     const int err = plan.exact ? sdf::launch_frames_exact(fa, plan.variant, blocks, stream)
                                : sdf::launch_frames_fast(fa, plan.variant, blocks, stream);
     if (err != hipSuccess) return SDF_E_HIP;
+    if (hipEventRecord(ds->done[slot], (hipStream_t)stream) != hipSuccess) return SDF_E_HIP;
+    ds->used[slot] = true;
   }
   return SDF_OK;
 }

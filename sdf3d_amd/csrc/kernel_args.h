@@ -73,7 +73,8 @@ struct KernelArgs {
 // one work counter, frame after frame, so a frame's slowest tiles overlap the
 // next frame's first ones instead of ending a launch.  The per-frame uniforms
 // ride in the kernel-argument segment beside the shared KernelArgs (whose own
-// camera and output fields are unused): 1,872 + 16 x 104 bytes.
+// camera and output fields are unused): sizeof(KernelArgs) + 16 x 104 bytes,
+// checked below against the 4 KiB explicit kernel-argument limit.
 constexpr int kFramesPerLaunch = 16;
 struct FrameCam {
   float inv_view[16];   // inverse(V_mat) of this frame's camera
@@ -93,6 +94,10 @@ struct FramesArgs {
   int32_t chunk;            // tiles per queue request (kChunkTiles)
   uint32_t* counter;        // queue q's counter at counter[q * kQueueStride], zero at launch
 };
+// the by-value kernel argument must fit the 4 KiB kernarg limit:
+// raising kMaxAoTaps, SDF_MAX_PRIMS or kFramesPerLaunch fails here, not at launch
+static_assert(sizeof(FramesArgs) <= 4096, "FramesArgs exceeds the 4 KiB kernel-argument limit");
+static_assert(sizeof(KernelArgs) <= 4096, "KernelArgs exceeds the 4 KiB kernel-argument limit");
 // Tiles a wave takes per queue request, queues per launch (workgroup b uses
 // queue b % queues, i.e. one per XCD), and the queues' spacing in uint32s:
 // requests on one address serialise at the memory-side atomic unit, so the

@@ -124,6 +124,18 @@ void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
     sdf_primitive& o = out[i];
     o.reserved = in.k > 0.0f ? 1.0f / in.k : 0.0f;
     o.p[11] = in.k * 0.25f;  // smooth-min k/4 (fast precision)
+    // exact precision's smooth-min division n / k (render_kernel.inc smin,
+    // cr_math.h div_scaled): sc = 2^s with k sc in [1, 2) (s <= 127, so a
+    // denormal k lands in [2^-22, 2)), and RN(1/(k sc)) by an IEEE division
+    float sc = 1.0f, ks = 1.0f;
+    if (in.k > 0.0f && std::isfinite(in.k)) {
+      int e = 0;
+      (void)std::frexp(in.k, &e);                 // k = m 2^e, m in [0.5, 1)
+      sc = std::ldexp(1.0f, std::min(1 - e, 127));
+      ks = in.k * sc;                             // exact
+    }
+    o.p[9] = sc;
+    o.p[10] = 1.0f / ks;
     const float* q = in.p;
     float* p = o.p;
     switch (in.kind) {

@@ -1,6 +1,6 @@
 // shmcomm.cpp -- TEST INFRASTRUCTURE ONLY: a stand-in for the RCCL symbols the
 // native frame driver loads at run time (sdf3d_amd/csrc/driver.cpp load_rccl:
-// ncclGetUniqueId, ncclCommInitRank, ncclCommDestroy, ncclCommAbort,
+// ncclGetUniqueId, ncclCommInitRank(Config), ncclCommDestroy, ncclCommAbort,
 // ncclCommGetAsyncError, ncclAllGather, ncclSend, ncclRecv, ncclGroupStart,
 // ncclGroupEnd), so that the driver's multi-rank sequence can run with
 // several ranks on ONE GPU, which RCCL refuses ("Duplicate GPU detected").
@@ -270,6 +270,14 @@ ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int 
   if (rank == 0) shm_unlink(c->name.c_str());  // every rank has it mapped
   *out = c;
   return ncclSuccess;
+}
+
+// The driver creates communicators through this entry point when it exists
+// (non-blocking, polled with ncclCommGetAsyncError): here creation completes
+// before returning, so the state it polls is ncclSuccess at once.
+ncclResult_t ncclCommInitRankConfig(ncclComm_t* out, int nranks, ncclUniqueId id, int rank,
+                                    ncclConfig_t*) {
+  return ncclCommInitRank(out, nranks, id, rank);
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t c) {

@@ -1,0 +1,61 @@
+"""The exact kernel's correctly rounded building blocks (sdf3d_amd/csrc/
+cr_math.h), checked EXHAUSTIVELY on the GPU by tests/crmath/crmath_check.hip:
+
+  * cr_sqrt(x) is bit-identical to IEEE sqrtf(x) for all 2^32 inputs (the
+    oracle's sqrtf; voxel_fragment.frag's length() / sqrt);
+  * rcp_fast(x) is bit-identical to IEEE 1.0f / x on its domain [2^-100,
+    2^100) (the Mandelbulb's 1 / sqrt(k3), k3 in [1e-30, 4]);
+  * cr_log(x) is bit-identical to (float)log((double)x) -- the oracle's
+    cr_logf (oracle/sdf_oracle.c), the Mandelbulb DE's log -- for all 2^32
+    inputs;
+  * the smooth-min's h = n / k by div_scaled: its bits equal IEEE n / k, or
+    (only where h < 2^-78) h*h*k/4 does, over 2^32 (k, n) pairs with k
+    log-uniform over every positive exponent and n over [0, k].
+
+With those, the exact-precision kernel stays bit-exact with the oracle
+(test_gpu_parity.py's full-size exact cases)."""
+import json
+import subprocess
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+EXE = Path(__file__).resolve().parent / "crmath" / "crmath_check"
+
+
+@pytest.fixture(scope="module")
+def results():
+    assert EXE.exists(), "build() must produce tests/crmath/crmath_check"
+    r = subprocess.run([str(EXE)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    out = Path("gpurun_out")
+    out.mkdir(exist_ok=True)
+    (out / "crmath_check.json").write_text(json.dumps(d, indent=1))
+    print(json.dumps(d))
+    return d
+
+
+def test_cr_sqrt_is_ieee_sqrt_everywhere(results):
+    r = results["sqrt"]
+    assert r["inputs"] == 2**32 and r["mismatch"] == 0, r
+    # the fast path covers [2^-100, 2^100): 200 binades of 2^23 floats
+    assert r["fast_path"] == 200 * 2**23, r
+
+
+def test_rcp_fast_is_ieee_reciprocal_on_its_domain(results):
+    r = results["rcp"]
+    assert r["fast_path"] == 200 * 2**23 and r["mismatch"] == 0, r
+
+
+def test_cr_log_is_the_oracles_log_everywhere(results):
+    r = results["log"]
+    assert r["inputs"] == 2**32 and r["mismatch"] == 0, r
+    # almost every positive normal float takes the fast path
+    assert r["fast_path"] > 0.999 * 254 * 2**23, r
+
+
+def test_smooth_min_division_is_bit_identical_where_it_counts(results):
+    r = results["smin"]
+    assert r["effective"] == 0, r
