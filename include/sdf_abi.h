@@ -126,7 +126,7 @@ typedef struct {
   float bulb_center[3];
   float bulb_scale;
   int32_t bulb_iterations;     /* default 12                                   */
-  float bulb_bailout;          /* default 2                                    */
+  float bulb_bailout;          /* default 2; (0, 2^32]                         */
   int32_t reserved[2];
 } sdf_scene;
 

@@ -593,7 +593,11 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   } else if (scene->kind == SDF_SCENE_MANDELBULB) {
     if (!(scene->bulb_scale > 0.0f) || !finite3(scene->bulb_center)) return SDF_E_INVALID_ARG;
     if (scene->bulb_iterations < 1 || scene->bulb_iterations > 64) return SDF_E_INVALID_ARG;
-    if (!(scene->bulb_bailout > 0.0f)) return SDF_E_INVALID_ARG;
+    // bailout in (0, 2^32]: its square stays finite, so every iteration's
+    // x^2 + z^2 <= m <= bailout^2 is finite (the exact kernel's 1 / sqrt of it,
+    // render_kernel.inc frsqrt, relies on that)
+    if (!(scene->bulb_bailout > 0.0f && scene->bulb_bailout <= 4294967296.0f))
+      return SDF_E_INVALID_ARG;
   } else {
     return SDF_E_INVALID_ARG;
   }

@@ -238,3 +238,13 @@ def test_strerror():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         abi.load_library(tmp_path / "nope.so")
+
+
+@pytest.mark.parametrize("bailout,ok", [(2.0, True), (2.0**32, True), (0.0, False), (-1.0, False),
+                                        (2.0**33, False), (float("inf"), False),
+                                        (float("nan"), False)])
+def test_validate_mandelbulb_bailout(bailout, ok):
+    """bailout in (0, 2^32]: its square stays finite (sdf_abi.h sdf_scene)."""
+    f = scenes.config("C5", 64, 36)
+    f.scene.bulb_bailout = bailout
+    assert _validate(f) == (abi.SDF_OK if ok else abi.SDF_E_INVALID_ARG)

@@ -148,3 +148,51 @@ def test_bounds_refusals():
     g.scene.prims[3].p[0] = float("nan")
     rc, *_ = bounds_of(g.scene)
     assert rc == abi.SDF_E_INVALID_ARG
+
+
+@pytest.mark.parametrize("kind", [abi.PRIM_SPHERE, abi.PRIM_BOX, abi.PRIM_ROUND_BOX,
+                                  abi.PRIM_TORUS, abi.PRIM_CAPSULE, abi.PRIM_CYLINDER])
+def test_primitive_solid_lies_inside_its_sphere(kind):
+    """Geometric check, independent of any radius formula: points
+    where the ORACLE's own SDF of the primitive is <= 0 (the solid) must lie
+    inside the bound the kernel culls with -- including rounded boxes whose
+    rounding radius exceeds a half extent (r > b on some axes, the branch the
+    round-box sphere |max(b - r, 0)| + r clamps)."""
+    import oracle
+    rng = np.random.default_rng(1000 + kind)
+    checked = 0
+    for trial in range(12):
+        f = scenes.config("C3", 64, 64)
+        s = f.scene
+        C.memset(C.addressof(s.prims), 0, C.sizeof(s.prims))
+        s.count = 2
+        s.prims[0].kind, s.prims[0].op = abi.PRIM_PLANE, abi.OP_UNION
+        s.prims[0].p[1], s.prims[0].p[3] = 1.0, 1e3      # far below: never the minimum
+        pr = s.prims[1]
+        pr.kind, pr.op, pr.k = kind, abi.OP_SMOOTH_UNION, 0.05
+        for j in range(3):
+            pr.p[j] = float(rng.uniform(-1, 1))
+        if kind == abi.PRIM_CAPSULE:
+            for j in range(3, 6):
+                pr.p[j] = float(rng.uniform(-1, 1))
+            pr.p[6] = float(rng.uniform(0.02, 0.4))
+        else:
+            for j in range(3, 6):
+                pr.p[j] = float(rng.uniform(0.05, 0.6))
+            if kind == abi.PRIM_ROUND_BOX:
+                # r beyond the smallest half extent on alternate trials
+                bmin = min(pr.p[3], pr.p[4], pr.p[5])
+                pr.p[6] = float(rng.uniform(1.05, 2.0) * bmin if trial % 2 else
+                                rng.uniform(0.0, 0.9) * bmin)
+        rc, b, cl, first = bounds_of(s)
+        assert rc == 0 and first == 1
+        cen, K = b[1, :3], b[1, 3]
+        R = K * (1 - REL) - ABS - pr.k          # the radius the bound encloses
+        ext = 2.5
+        pts = rng.uniform(-ext, ext, size=(6000, 3)) + np.array(pr.p[0:3])
+        # the primitive alone: the plane term is 1e3 above every sample
+        inside = [p for p in pts if oracle.scene_sdf(s, *map(float, p)) <= 0.0]
+        for p in inside:
+            assert np.linalg.norm(p - cen) <= R * (1 + 1e-6) + 1e-6, (kind, trial, p, R)
+        checked += len(inside)
+    assert checked > 100, checked
