@@ -151,8 +151,16 @@ static inline REAL FN(mandelbulb)(FN(v3) q, int iters, REAL bail2) {
                     (xn4 * xn4 - (REAL)28 * xn4 * xn2 * zn2 + (REAL)70 * xn4 * zn4 -
                      (REAL)28 * xn2 * zn2 * zn4 + zn4 * zn4) * s;
     m = FN(dot)(w, w);
-    if (m > bail2) break;
+    if (m > bail2) {
+#ifdef ORACLE_BULB_ITER_HOOK
+      ORACLE_BULB_ITER_HOOK(i + 1);
+#endif
+      return (REAL)0.25 * LOG(m) * SQRT(m) / dz;
+    }
   }
+#ifdef ORACLE_BULB_ITER_HOOK
+  ORACLE_BULB_ITER_HOOK(iters);
+#endif
   return (REAL)0.25 * LOG(m) * SQRT(m) / dz;
 }
 
@@ -168,7 +176,12 @@ static REAL FN(scene_sdf)(const sdf_scene* s, FN(v3) p) {
      * least |q| - 1.25 away: return that bound (keeps the polynomial DE away
      * from fp32 overflow far from the set). */
     REAL m0 = FN(dot)(q, q);
-    if (m0 > (REAL)2.25) return (SQRT(m0) - (REAL)1.25) * sc;
+    if (m0 > (REAL)2.25) {
+#ifdef ORACLE_BULB_ITER_HOOK
+      ORACLE_BULB_ITER_HOOK(0);   /* outside the bounding sphere: no map iterations */
+#endif
+      return (SQRT(m0) - (REAL)1.25) * sc;
+    }
     REAL bail = s->bulb_bailout;
     return FN(mandelbulb)(q, s->bulb_iterations, bail * bail) * sc;
   }
@@ -322,6 +335,9 @@ static void FN(shade_pixel)(const sdf_scene* s, const sdf_light* li,
     FN(v3) o = FN(mk)(P.x + N.x * off * eps, P.y + N.y * off * eps, P.z + N.z * off * eps);
     sh = FN(shadow_n)(s, pa, o, incident, (REAL)pa->shadow_k, force ? force[1] : -1, &ss);
   }
+#ifdef ORACLE_PIXEL_HOOK
+  ORACLE_PIXEL_HOOK(FN(dot)(N, incident) > 0);   /* instrumentation (tools/) only */
+#endif
   REAL dif = FN(gclamp)(FN(dot)(N, incident), 0, 1) * sh;         /* :205 */
   REAL la = li->ambient;
   REAL amb[3] = {la * (REAL)M->amb[0], la * (REAL)M->amb[1], la * (REAL)M->amb[2]}; /* :206 */
