@@ -6,20 +6,39 @@
 // several ranks on ONE GPU, which RCCL refuses ("Duplicate GPU detected").
 //
 // Every rank is a process; a communicator is one POSIX shared-memory segment
-// named by the unique id.  Data moves through host memory:
-//   * a call first waits for the work already enqueued on its stream
-//     (hipStreamSynchronize), as the collective would be ordered after it,
-//   * then copies device -> shared memory -> device on a private stream and
-//     returns with the data in place, so later work on the stream sees it.
-// So every call completes on the host before it returns (stricter than
-// RCCL's asynchronous enqueue, never weaker): a dependency the driver forgets
-// on ANOTHER stream (a render on rs[b] not waited for before a send on ds)
-// still shows as a wrong frame.  Sends and receives inside a group are
+// named by the unique id.  Data moves through host memory.
+//
+// ASYNCHRONOUS, like RCCL (round 3; VERDICT r02: the round-2 stand-in
+// completed every call before returning, so it could not show a missing
+// stream dependency or a cross-communicator ordering hazard).  A call returns
+// as soon as it is enqueued:
+//   * it records an event on the caller's stream (the work the collective is
+//     ordered after) and makes the stream wait, on the GPU, for the call's
+//     completion flag (hipStreamWaitValue32 on coherent host memory);
+//   * ONE progress engine per process runs the calls of ALL its
+//     communicators in the order they were issued: it waits for the call's
+//     event, moves the data (device -> shared memory -> device, on a private
+//     stream), then writes the flag (a host store to coherent memory),
+//     releasing the caller's stream.
+// So the driver's streams see RCCL's ordering (nothing after a collective on
+// its stream runs before the collective's data is in place; nothing else is
+// ordered), and the single FIFO engine is STRICTER than RCCL across
+// communicators: ranks that issue calls on two communicators in different
+// orders deadlock here and hit the time limit, so every rank must issue its
+// calls in one global order.  Sends and receives inside a group are
 // progressed together, chunk by chunk, so any pattern (rank 0 receiving from
 // 7 peers, a rank sending to itself) completes.  Every wait polls with a
 // limit (SHMCOMM_TIMEOUT_MS, default 60 s) and then sets the communicator's
-// asynchronous error, as a failed RCCL would.  Never linked into the product
-// library; tests load it through the driver's rccl_path.
+// asynchronous error, as a failed RCCL would -- and still writes the flag, so
+// no GPU stream is left waiting.  A stream held by a wait packet holds the
+// hardware queue it sits on, so every stream of a test process needs a queue
+// of its own, as on real hardware for RCCL's spinning kernels: the tests run
+// with GPU_MAX_HW_QUEUES=8 (as bench.py's N > 1 runs) or 16; a rank holds
+// the default stream, its render streams, the driver's two communication
+// streams and this library's one copy stream.  SHMCOMM_SYNC=1 (or a device without
+// stream wait-value support) selects the round-2 behaviour: each call waits
+// for its stream and completes before returning.  Never linked into the
+// product library; tests load it through the driver's rccl_path.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types and signatures only
@@ -29,11 +48,17 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -91,7 +116,7 @@ struct ncclComm {
   uint64_t ag_ops = 0;
   std::vector<uint64_t> sent, taken;  // my view: chunks I sent to / took from each peer
   hipStream_t copy = nullptr;
-  ncclResult_t async = ncclSuccess;
+  std::atomic<int> async{ncclSuccess};
   long timeout_ms = 60000;
 
   Header* hdr() { return reinterpret_cast<Header*>(base); }
@@ -108,7 +133,6 @@ struct ncclComm {
 namespace {
 
 thread_local int g_group_depth = 0;
-thread_local std::vector<std::pair<ncclComm*, std::vector<Op>>> g_group;
 
 using Clock = std::chrono::steady_clock;
 
@@ -126,18 +150,41 @@ bool wait_for(ncclComm* c, Pred ready) {
     }
     sched_yield();
   }
-  c->async = ncclSystemError;
+  c->async.store(ncclSystemError);
   return false;
+}
+
+// ONE copy stream per process, shared by all communicators (only the engine
+// thread, or in synchronous mode the calling thread, uses it): the fewer
+// streams a rank holds, the fewer hardware queues it needs
+hipStream_t copy_stream() {
+  static std::mutex mu;
+  static hipStream_t s = nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!s) (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  return s;
 }
 
 bool copy(ncclComm* c, void* dst, const void* src, size_t n, hipMemcpyKind kind) {
   if (n == 0) return true;
-  if (hipMemcpyAsync(dst, src, n, kind, c->copy) != hipSuccess ||
-      hipStreamSynchronize(c->copy) != hipSuccess) {
-    c->async = ncclUnhandledCudaError;
+  if (hipMemcpyAsync(dst, src, n, kind, c->copy) != hipSuccess) {
+    c->async.store(ncclUnhandledCudaError);
     return false;
   }
-  return true;
+  // polled with the limit: a copy stream that shares a hardware queue with a
+  // stream held by a wait-value packet would otherwise block forever
+  const auto t0 = Clock::now();
+  for (unsigned k = 0;; ++k) {
+    const hipError_t q = hipStreamQuery(c->copy);
+    if (q == hipSuccess) return true;
+    if (q != hipErrorNotReady ||
+        std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - t0).count() >
+            c->timeout_ms) {
+      c->async.store(ncclUnhandledCudaError);
+      return false;
+    }
+    if ((k & 63) == 63) sched_yield();
+  }
 }
 
 size_t dtype_size(ncclDataType_t t) {
@@ -187,36 +234,204 @@ ncclResult_t run_ops(ncclComm* c, std::vector<Op>& ops) {
     all = true;
     for (Op& op : ops) {
       progress(c, op);
-      if (c->async != ncclSuccess) return true;
+      if (c->async.load() != ncclSuccess) return true;
       all = all && op.chunk == op.nchunks;
     }
     return all;
   };
-  if (!wait_for(c, finished) || c->async != ncclSuccess) return ncclSystemError;
+  if (!wait_for(c, finished) || c->async.load() != ncclSuccess) return ncclSystemError;
   return ncclSuccess;
 }
 
+// ---- the progress engine (one per process) ---------------------------------
+constexpr uint32_t kFlags = 4096;   // completion flags, slot seq % kFlags
+
+struct Task {
+  std::vector<hipEvent_t> ready;   // the callers' streams up to the call
+  std::function<ncclResult_t()> run;
+  std::vector<ncclComm*> comms;
+  uint32_t seq = 0;
+};
+
+struct Engine {
+  std::mutex mu;
+  std::condition_variable cv, idle;
+  std::deque<Task> q;
+  bool busy = false;
+  int dev = 0;
+  uint32_t* flags = nullptr;   // coherent pinned host memory
+  uint32_t seq = 0;
+  long timeout_ms = 60000;
+};
+
+Engine* g_engine = nullptr;   // never destroyed: its thread may outlive main's locals
+int g_engine_state = 0;       // 1 engine, -1 SHMCOMM_SYNC, -2 no wait-value support, -3 setup
+std::mutex g_engine_mu;
+
+bool async_mode() {
+  const char* e = std::getenv("SHMCOMM_SYNC");
+  return !(e && *e && *e != '0');
+}
+
+void engine_loop(Engine* E) {
+  (void)hipSetDevice(E->dev);
+  for (;;) {
+    Task t;
+    {
+      std::unique_lock<std::mutex> lock(E->mu);
+      E->cv.wait(lock, [&] { return !E->q.empty(); });
+      t = std::move(E->q.front());
+      E->q.pop_front();
+      E->busy = true;
+    }
+    // the work the call is ordered after, with the communicators' limit
+    bool ok = true;
+    const auto t0 = Clock::now();
+    for (hipEvent_t ev : t.ready) {
+      for (unsigned n = 0;; ++n) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady ||
+            std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - t0).count() >
+                E->timeout_ms) {
+          ok = false;
+          break;
+        }
+        if ((n & 63) == 63) sched_yield();
+      }
+      (void)hipEventDestroy(ev);
+    }
+    const ncclResult_t rc = ok ? t.run() : ncclSystemError;
+    if (rc != ncclSuccess)
+      for (ncclComm* c : t.comms) {
+        int expect = ncclSuccess;
+        c->async.compare_exchange_strong(expect, rc == ncclInProgress ? ncclSystemError : rc);
+      }
+    // release the callers' streams whatever happened (no stream left waiting):
+    // a host store to the coherent flag the GPU's wait packet polls, so the
+    // release needs no queue of its own
+    __atomic_store_n(E->flags + t.seq % kFlags, t.seq, __ATOMIC_RELEASE);
+    {
+      std::lock_guard<std::mutex> lock(E->mu);
+      E->busy = false;
+      if (E->q.empty()) E->idle.notify_all();
+    }
+  }
+}
+
+// The process's engine, created on the calling thread's device; null when
+// the device cannot wait on a value (then calls run synchronously).
+Engine* engine(long timeout_ms) {
+  if (!async_mode()) {
+    g_engine_state = -1;
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(g_engine_mu);
+  if (g_engine) return g_engine;
+  int dev = 0, can = 0;
+  const bool dbg = std::getenv("SHMCOMM_DEBUG") != nullptr;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess ||
+      !can) {
+    if (dbg) std::fprintf(stderr, "shmcomm: no stream wait-value support (%d): synchronous\n", can);
+    g_engine_state = -2;
+    return nullptr;
+  }
+  auto* E = new Engine;
+  E->dev = dev;
+  E->timeout_ms = timeout_ms;
+  // coherent pinned host memory: the GPU's wait-value and write-value packets
+  // both work on it (hipMallocSignalMemory takes single 8-byte signals only)
+  if (hipHostMalloc(reinterpret_cast<void**>(&E->flags), kFlags * sizeof(uint32_t),
+                    hipHostMallocCoherent) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    if (dbg) std::fprintf(stderr, "shmcomm: engine setup failed: synchronous\n");
+    g_engine_state = -3;
+    delete E;
+    return nullptr;
+  }
+  std::memset(E->flags, 0, kFlags * sizeof(uint32_t));
+  std::thread(engine_loop, E).detach();
+  g_engine = E;
+  g_engine_state = 1;
+  return E;
+}
+
+// Enqueue `run` after the work already on `streams`; the streams wait (on the
+// GPU) for its completion.  Without an engine: wait for the streams, run now.
+ncclResult_t submit(std::vector<hipStream_t> streams, std::vector<ncclComm*> comms,
+                    std::function<ncclResult_t()> run) {
+  Engine* E = engine(comms.empty() ? 60000 : comms[0]->timeout_ms);
+  if (!E) {
+    for (hipStream_t s : streams)
+      if (hipStreamSynchronize(s) != hipSuccess) return ncclUnhandledCudaError;
+    return run();
+  }
+  Task t;
+  t.run = std::move(run);
+  t.comms = std::move(comms);
+  for (hipStream_t s : streams) {
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(ev, s) != hipSuccess)
+      return ncclUnhandledCudaError;
+    t.ready.push_back(ev);
+  }
+  std::lock_guard<std::mutex> lock(E->mu);
+  t.seq = ++E->seq;
+  for (hipStream_t s : streams)
+    if (hipStreamWaitValue32(s, E->flags + t.seq % kFlags, t.seq, hipStreamWaitValueGte) !=
+        hipSuccess)
+      return ncclUnhandledCudaError;
+  E->q.push_back(std::move(t));
+  E->cv.notify_one();
+  return ncclSuccess;
+}
+
+// Wait until the engine has run every call enqueued so far (communicator
+// teardown: nothing of it may still be in use).
+void engine_drain(long timeout_ms) {
+  Engine* E = g_engine;
+  if (!E) return;
+  std::unique_lock<std::mutex> lock(E->mu);
+  E->idle.wait_for(lock, std::chrono::milliseconds(timeout_ms + 1000),
+                   [&] { return E->q.empty() && !E->busy; });
+}
+
+struct GroupEntry {
+  ncclComm* comm;
+  std::vector<Op> ops;
+  std::vector<hipStream_t> streams;
+};
+thread_local std::vector<GroupEntry> g_pending;
+
 ncclResult_t enqueue(ncclComm* c, Op op, hipStream_t stream) {
-  if (!c || c->async != ncclSuccess) return ncclInvalidUsage;
+  if (!c || c->async.load() != ncclSuccess) return ncclInvalidUsage;
   if (op.peer < 0 || op.peer >= c->nranks) return ncclInvalidArgument;
-  // ordered after the work already on `stream`
-  if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
   if (g_group_depth > 0) {
-    for (auto& g : g_group)
-      if (g.first == c) {
-        g.second.push_back(op);
+    for (auto& g : g_pending)
+      if (g.comm == c) {
+        g.ops.push_back(op);
+        bool have = false;
+        for (hipStream_t s : g.streams) have = have || s == stream;
+        if (!have) g.streams.push_back(stream);
         return ncclSuccess;
       }
-    g_group.push_back({c, {op}});
+    g_pending.push_back({c, {op}, {stream}});
     return ncclSuccess;
   }
-  std::vector<Op> ops{op};
-  return run_ops(c, ops);
+  return submit({stream}, {c}, [c, op]() mutable {
+    std::vector<Op> ops{op};
+    return run_ops(c, ops);
+  });
 }
 
 }  // namespace
 
 extern "C" {
+
+// 1 when calls run on the asynchronous engine, 0 when synchronously (tests)
+int shmcomm_async_engine(void) { return g_engine_state; }
 
 ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
   if (!id) return ncclInvalidArgument;
@@ -259,7 +474,15 @@ ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int 
   c->hdr()->nranks = nranks;
   c->sent.assign(nranks, 0);
   c->taken.assign(nranks, 0);
-  (void)hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  c->copy = copy_stream();
+  // created now (its setup synchronises the device); SHMCOMM_REQUIRE_ASYNC=1
+  // makes a missing engine an error, so a test cannot pass synchronously
+  if (!engine(c->timeout_ms) && std::getenv("SHMCOMM_REQUIRE_ASYNC")) {
+    munmap(c->base, c->size);
+    delete c->L;
+    delete c;
+    return ncclSystemError;
+  }
   c->hdr()->joined.fetch_add(1);
   if (!wait_for(c, [&] { return c->hdr()->joined.load() >= nranks; })) {
     munmap(c->base, c->size);
@@ -282,7 +505,8 @@ ncclResult_t ncclCommInitRankConfig(ncclComm_t* out, int nranks, ncclUniqueId id
 
 ncclResult_t ncclCommDestroy(ncclComm_t c) {
   if (!c) return ncclSuccess;
-  if (c->copy) (void)hipStreamDestroy(c->copy);
+  engine_drain(c->timeout_ms);   // no call of it still running
+  // (the copy stream is the process's, shared by its communicators)
   munmap(c->base, c->size);
   delete c->L;
   delete c;
@@ -297,38 +521,39 @@ ncclResult_t ncclCommAbort(ncclComm_t c) {
 
 ncclResult_t ncclCommGetAsyncError(ncclComm_t c, ncclResult_t* e) {
   if (!c || !e) return ncclInvalidArgument;
-  *e = c->hdr()->aborted.load() ? ncclRemoteError : c->async;
+  *e = c->hdr()->aborted.load() ? ncclRemoteError : (ncclResult_t)c->async.load();
   return ncclSuccess;
 }
 
 ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t count,
                            ncclDataType_t datatype, ncclComm_t c, hipStream_t stream) {
-  if (!c || c->async != ncclSuccess) return ncclInvalidUsage;
+  if (!c || c->async.load() != ncclSuccess) return ncclInvalidUsage;
   const size_t bytes = count * dtype_size(datatype);
   if (bytes > kAgBytes) return ncclInvalidArgument;
-  if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
-  const uint64_t k = c->ag_ops++;
-  const int slot = int(k % kAgSlots);
-  // the slot is free once every rank has finished all-gather k - kAgSlots
-  if (!wait_for(c, [&] {
-        for (int r = 0; r < c->nranks; ++r)
-          if (k >= kAgSlots && c->ag(r)->done.load(std::memory_order_acquire) < k - kAgSlots + 1)
-            return false;
-        return true;
-      }))
-    return ncclSystemError;
-  if (!copy(c, c->ag_buf(slot, c->rank), sendbuff, bytes, hipMemcpyDeviceToHost))
-    return ncclUnhandledCudaError;
-  c->ag(c->rank)->seq[slot].store(k + 1, std::memory_order_release);
-  for (int r = 0; r < c->nranks; ++r) {
-    if (!wait_for(c, [&] { return c->ag(r)->seq[slot].load(std::memory_order_acquire) == k + 1; }))
+  const uint64_t k = c->ag_ops++;   // issue order = the engine's order
+  return submit({stream}, {c}, [c, k, bytes, sendbuff, recvbuff]() -> ncclResult_t {
+    const int slot = int(k % kAgSlots);
+    // the slot is free once every rank has finished all-gather k - kAgSlots
+    if (!wait_for(c, [&] {
+          for (int r = 0; r < c->nranks; ++r)
+            if (k >= kAgSlots && c->ag(r)->done.load(std::memory_order_acquire) < k - kAgSlots + 1)
+              return false;
+          return true;
+        }))
       return ncclSystemError;
-    if (!copy(c, static_cast<char*>(recvbuff) + r * bytes, c->ag_buf(slot, r), bytes,
-              hipMemcpyHostToDevice))
+    if (!copy(c, c->ag_buf(slot, c->rank), sendbuff, bytes, hipMemcpyDeviceToHost))
       return ncclUnhandledCudaError;
-  }
-  c->ag(c->rank)->done.store(k + 1, std::memory_order_release);
-  return ncclSuccess;
+    c->ag(c->rank)->seq[slot].store(k + 1, std::memory_order_release);
+    for (int r = 0; r < c->nranks; ++r) {
+      if (!wait_for(c, [&] { return c->ag(r)->seq[slot].load(std::memory_order_acquire) == k + 1; }))
+        return ncclSystemError;
+      if (!copy(c, static_cast<char*>(recvbuff) + r * bytes, c->ag_buf(slot, r), bytes,
+                hipMemcpyHostToDevice))
+        return ncclUnhandledCudaError;
+    }
+    c->ag(c->rank)->done.store(k + 1, std::memory_order_release);
+    return ncclSuccess;
+  });
 }
 
 ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
@@ -351,14 +576,29 @@ ncclResult_t ncclGroupStart() {
 ncclResult_t ncclGroupEnd() {
   if (g_group_depth <= 0) return ncclInvalidUsage;
   if (--g_group_depth > 0) return ncclSuccess;
-  ncclResult_t rc = ncclSuccess;
-  auto groups = std::move(g_group);
-  g_group.clear();
+  auto groups = std::move(g_pending);
+  g_pending.clear();
+  if (groups.empty()) return ncclSuccess;
+  // one call for the whole group: every stream in it waits for all of it
+  std::vector<hipStream_t> streams;
+  std::vector<ncclComm*> comms;
   for (auto& g : groups) {
-    const ncclResult_t r = run_ops(g.first, g.second);
-    if (rc == ncclSuccess) rc = r;
+    comms.push_back(g.comm);
+    for (hipStream_t s : g.streams) {
+      bool have = false;
+      for (hipStream_t t : streams) have = have || t == s;
+      if (!have) streams.push_back(s);
+    }
   }
-  return rc;
+  auto shared = std::make_shared<std::vector<GroupEntry>>(std::move(groups));
+  return submit(streams, comms, [shared]() {
+    ncclResult_t rc = ncclSuccess;
+    for (auto& g : *shared) {
+      const ncclResult_t r = run_ops(g.comm, g.ops);
+      if (rc == ncclSuccess) rc = r;
+    }
+    return rc;
+  });
 }
 
 }  // extern "C"

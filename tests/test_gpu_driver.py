@@ -137,7 +137,10 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
     all-gather, send/recv of the TILES streams to rank 0, decode) with
     `nproc` ranks sharing this GPU: bench.py --driver native over the
     stand-in communications library tests/shmcomm (RCCL refuses two ranks on
-    one GPU).  Rank 0's assembled last frame must equal a single-device
+    one GPU), in its asynchronous mode (required): calls return once
+    enqueued and hold only their own stream, on the GPU, until the data is in
+    place, and one FIFO engine per rank makes any cross-communicator order
+    mismatch between ranks an error.  Rank 0's assembled last frame must equal a single-device
     render bit for bit; the 8-rank C4 case is the round-end N = 8 bench's
     configuration (4K, default 1:3 shares)."""
     import json
@@ -151,7 +154,8 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
            "--config", cfg, "--no-display", "--clock-warm-s", "0"]
     if shares:
         cmd += ["--shares", shares]
-    env = dict(os.environ, SHMCOMM_TIMEOUT_MS="60000")
+    env = dict(os.environ, SHMCOMM_TIMEOUT_MS="60000", GPU_MAX_HW_QUEUES="8",
+                   SHMCOMM_REQUIRE_ASYNC="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -196,7 +200,8 @@ def test_cpp_driver_multirank_arcball(tmp_path, world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
                    SDF3D_RCCL=str(SHMCOMM), SDF3D_ID_DIR=str(tmp_path),
                    SDF3D_RUN_ID=f"t{os.getpid()}_{world}", SDF3D_NAV="arcball",
-                   SHMCOMM_TIMEOUT_MS="60000", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+                   SHMCOMM_TIMEOUT_MS="60000", GPU_MAX_HW_QUEUES="8",
+                   SHMCOMM_REQUIRE_ASYNC="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([str(exe), str(W), str(H), str(frames), str(out), "csg8"],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                       text=True))

@@ -1,0 +1,45 @@
+"""The asynchronous stand-in communications library (tests/shmcomm), the
+substrate of the native driver's multi-rank tests (test_gpu_driver.py):
+its calls return once enqueued, like RCCL's, with the caller's stream held
+on the GPU until the data is in place; and its single per-process FIFO
+engine turns ranks that issue calls on two communicators in different orders
+into a reported error (SHMCOMM_TIMEOUT_MS), never a hang."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = Path(__file__).resolve().parent
+PROBE = HERE / "shmcomm" / "order_probe.py"
+
+
+def run_pair(tmp_path, mode, timeout_ms):
+    # every stream its own hardware queue (tests/shmcomm/shmcomm.cpp)
+    env = dict(os.environ, SHMCOMM_TIMEOUT_MS=str(timeout_ms), GPU_MAX_HW_QUEUES="16")
+    env.pop("SHMCOMM_SYNC", None)
+    procs = [subprocess.Popen([sys.executable, str(PROBE), str(r), str(tmp_path), mode],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for r in range(2)]
+    outs = [p.communicate(timeout=150) for p in procs]
+    for p, (so, se) in zip(procs, outs):
+        assert p.returncode == 0, se[-2000:]
+    return [json.loads(so.strip().splitlines()[-1]) for so, _ in outs]
+
+
+def test_calls_are_asynchronous_and_correct(tmp_path):
+    for r in run_pair(tmp_path, "same", 30000):
+        assert r["correct"] and r["async_errors"] == [0, 0] and r["rcs"] == [0] * 6, r
+        # six all-gathers issued behind ~0.4-0.7 s of GPU work return at once
+        assert r["async_engine"] == 1, r
+        assert r["issue_s"] < 0.2 and r["drain_s"] > 0.2, r
+
+
+def test_crossed_communicator_order_is_an_error_not_a_hang(tmp_path):
+    res = run_pair(tmp_path, "crossed", 3000)
+    assert any(e != 0 for r in res for e in r["async_errors"]), res
+    for r in res:
+        assert r["drain_s"] < 60, r     # the streams were released
