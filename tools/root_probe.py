@@ -35,12 +35,15 @@ def main():
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--shares", default="1:1", help="rank 0 : other ranks, blocks per period")
     ap.add_argument("--streams", type=int, default=3, help="alternating streams / buffers")
+    ap.add_argument("--lib", default=None, help="another libsdf3d.so build (A/B)")
     ap.add_argument("--only", choices=["decode", "root", "peer"], default=None,
                     help="time one leg only (for rocprofv3 counter passes)")
     args = ap.parse_args()
     import torch
     from sdf3d_amd import Renderer, abi, renderer as R, scenes
     rd = Renderer("cuda:0")
+    if args.lib:
+        rd.lib = abi.load_library(args.lib)
     N, K = args.world, args.frames
     f = scenes.config(args.config, precision=abi.PRECISION_FAST)
     W, H = f.params.width, f.params.height
