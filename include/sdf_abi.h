@@ -56,8 +56,10 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 8   /* 7: sdf_comm_create timeout, sdf_render_multi;
-                                8: sdf_render_frames */
+#define SDF_ABI_VERSION 9   /* 7: sdf_comm_create timeout, sdf_render_multi;
+                                8: sdf_render_frames;
+                                9: TILES carries shading terms (64-byte
+                                   stream header), SDF_FORMAT_SHADE32F */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -202,9 +204,20 @@ typedef struct {
  *            writes as 1.0 (voxel_fragment.frag:210): a lossless 12-byte
  *            wire format for multi-device frames; sdf_deinterleave expands
  *            it to an RGBA32F frame with alpha = 1.
- *   TILES    RGB32F losslessly compressed for the multi-device gather (about
- *            3.2 instead of 12 bytes per pixel on the 4K CSG scene), decoded
- *            bit for bit by sdf_tiles_decode.  The rendered (packed) rows
+ *   SHADE32F the pixel's three shading terms instead of its colour, as
+ *            RGBA32F (ao, dif, x, 1): ao the AO factor (1 without AO), dif =
+ *            clamp(N.L, 0, 1) * shadow, x = max(N.H, 0); the colour is
+ *            la * amb * ao + dif * mat.dif + pow(x, shininess) * mat.ref
+ *            (voxel_fragment.frag:204-210) in the precision's fixed operation
+ *            sequence (sdf3d_amd/csrc/shade.h).  Diagnostics: what TILES
+ *            streams carry.
+ *   TILES    the frame losslessly compressed for the multi-device gather
+ *            (about 2.3 instead of 12 bytes per pixel on the 4K CSG scene),
+ *            decoded bit for bit by sdf_tiles_decode.  A rendered stream
+ *            carries the SHADE32F terms in its three channels (smoother than
+ *            the colour, which mixes them: 29 % fewer bytes) and the frame's
+ *            shading constants in its header; the decoder makes the colour
+ *            from them exactly as sdf_render does.  The rendered (packed) rows
  *            are cut into 8x8 tiles, tile t = ty * ceil(width / 8) + tx
  *            covering packed rows 8ty.. and columns 8tx..; pixel j = 8 *
  *            row + column of a tile.  Per tile and channel: the float bits
@@ -224,8 +237,17 @@ typedef struct {
  *            buffer, stream plus the encoder's scratch):
  *              u32 used             bytes of tile data
  *              u32 ntiles
- *              u32 offset[ntiles]   tile t's data at data + offset[t]
- *              head = stream + align16(8 + 4 * ntiles):
+ *              u32 shade            0: the channels are RGB (a stream not
+ *                                   made by sdf_render); 1 / 2: shading
+ *                                   terms of a fast / exact render
+ *              u32 0
+ *              f32 lam[3]           light.ambient * material.amb[c] (fp32)
+ *              f32 dif[3], ref[3]   material.dif, material.ref
+ *              f32 shininess
+ *              u32 0, 0
+ *              u32 offset[ntiles]   (at byte 64) tile t's data at data +
+ *                                   offset[t]
+ *              head = stream + align16(64 + 4 * ntiles):
  *                u32x4 head[ntiles] {b0 | b1 << 6 | b2 << 12 | q << 18 |
  *                                   e << 26, first[3]}: q the tile's data
  *                                   in u64 words, e bit c set when channel
@@ -248,7 +270,8 @@ typedef enum {
   SDF_FORMAT_RGBA16F = 1,
   SDF_FORMAT_RGBA8 = 2,
   SDF_FORMAT_RGB32F = 3,
-  SDF_FORMAT_TILES = 4
+  SDF_FORMAT_TILES = 4,
+  SDF_FORMAT_SHADE32F = 5
 } sdf_format;
 
 typedef enum {
@@ -320,7 +343,7 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera,
  * negative SDF_E* code. */
 int sdf_owned_rows(int32_t height, const sdf_tiling* tiling);
 
-/* Bytes per pixel of a sdf_format (16, 8, 4, 12), or a negative SDF_E* code
+/* Bytes per pixel of a sdf_format (16, 8, 4, 12, -, 16), or a negative SDF_E* code
  * (SDF_E_UNSUPPORTED for TILES, whose size is per stream). */
 int sdf_format_bytes(int32_t format);
 

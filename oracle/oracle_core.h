@@ -344,6 +344,11 @@ static void FN(shade_pixel)(const sdf_scene* s, const sdf_light* li,
   if ((pa->flags & SDF_FLAG_AO) && pa->ao_taps > 0) {
     REAL ao = FN(ambient_occlusion)(s, pa, P, N);
     amb[0] = amb[0] * ao; amb[1] = amb[1] * ao; amb[2] = amb[2] * ao;
+#ifdef ORACLE_TERMS_HOOK
+    ORACLE_TERMS_HOOK(ao, dif, spec, FN(gmax)(FN(dot)(N, halfway), 0), FN(gclamp)(FN(dot)(N, incident), 0, 1), sh);   /* instrumentation (tools/) only */
+  } else {
+    ORACLE_TERMS_HOOK(1, dif, spec, FN(gmax)(FN(dot)(N, halfway), 0), FN(gclamp)(FN(dot)(N, incident), 0, 1), sh);
+#endif
   }
   for (int c = 0; c < 3; c++)                                      /* :207-210 */
     out[c] = (float)(amb[c] + dif * (REAL)M->dif[c] + spec * (REAL)M->ref[c]);

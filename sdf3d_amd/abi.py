@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 8
+SDF_ABI_VERSION = 9
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -40,12 +40,15 @@ NORMAL_CENTRAL, NORMAL_TETRA = 0, 1
 PRECISION_EXACT, PRECISION_FAST = 0, 1
 DISPATCH_AUTO, DISPATCH_GENERIC, DISPATCH_UNCULLED = 0, 1, 2
 FORMAT_RGBA32F, FORMAT_RGBA16F, FORMAT_RGBA8, FORMAT_RGB32F, FORMAT_TILES = 0, 1, 2, 3, 4
+FORMAT_SHADE32F = 5   # the pixels' shading terms (ao, dif, x, 1): what TILES carries
 TILING_FRAME_ROWS = 1
 FORMAT_NAMES = {"rgba32f": FORMAT_RGBA32F, "rgba16f": FORMAT_RGBA16F, "rgba8": FORMAT_RGBA8,
-                "rgb32f": FORMAT_RGB32F}
-# TILES (lossless compressed RGB32F, the multi-device wire) is a byte stream
-# of per-frame length, not a pixel format: see Renderer.alloc
-FORMAT_CHANNELS = {FORMAT_RGBA32F: 4, FORMAT_RGBA16F: 4, FORMAT_RGBA8: 4, FORMAT_RGB32F: 3}
+                "rgb32f": FORMAT_RGB32F, "shade32f": FORMAT_SHADE32F}
+# TILES (the frame losslessly compressed, the multi-device wire) is a byte
+# stream of per-frame length, not a pixel format: see Renderer.alloc
+FORMAT_CHANNELS = {FORMAT_RGBA32F: 4, FORMAT_RGBA16F: 4, FORMAT_RGBA8: 4, FORMAT_RGB32F: 3,
+                   FORMAT_SHADE32F: 4}
+TILES_HEADER_BYTES = 64   # used, ntiles, shade mode, 0, shading constants (sdf_abi.h)
 
 
 class sdf_primitive(C.Structure):
@@ -173,8 +176,10 @@ def _strerror(code: int) -> str:
         return f"error {code}"
 
 
-def load_library(path: Path | str | None = None) -> C.CDLL:
-    """Load the in-tree HIP library; raise if it has not been built."""
+def load_library(path: Path | str | None = None, any_version: bool = False) -> C.CDLL:
+    """Load the in-tree HIP library; raise if it has not been built.
+    any_version: accept another ABI version (measurement tools timing an
+    older build of the same entry points side by side)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -189,7 +194,7 @@ def load_library(path: Path | str | None = None) -> C.CDLL:
         fn.restype = res
         fn.argtypes = args
     v = lib.sdf_abi_version()
-    if v != SDF_ABI_VERSION:
+    if v != SDF_ABI_VERSION and not any_version:
         raise RuntimeError(f"libsdf3d ABI version {v} != {SDF_ABI_VERSION}")
     if path is None:
         _lib = lib

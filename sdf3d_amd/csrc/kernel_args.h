@@ -141,13 +141,14 @@ int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, vo
 // slots.  sdf_tiles_bytes() = end.
 constexpr int kTilePlaneBytes = 8 * 96;   // 3 channels x 32 planes
 constexpr int kScanTiles = 2048;          // tiles per block of the offset scan
+constexpr int kTilesHeaderBytes = 64;     // used, ntiles, shade mode, 0, ShadeK, 0, 0
 struct TilesLayout {
   size_t table, head, data, stream_end, bsums, slots, end;
   __host__ __device__ explicit TilesLayout(long long ntiles) {
     const size_t n = (size_t)ntiles;
     const size_t nb = (n + kScanTiles - 1) / kScanTiles;
-    table = 8;
-    head = (8 + 4 * n + 15) & ~(size_t)15;
+    table = kTilesHeaderBytes;
+    head = (kTilesHeaderBytes + 4 * n + 15) & ~(size_t)15;
     data = head + 16 * n;
     stream_end = data + n * kTilePlaneBytes;
     bsums = (stream_end + 15) & ~(size_t)15;

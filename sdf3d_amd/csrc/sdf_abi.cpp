@@ -619,6 +619,7 @@ int sdf_format_bytes(int32_t format) {
     case SDF_FORMAT_RGBA8: return 4;
     case SDF_FORMAT_RGB32F: return 12;
     case SDF_FORMAT_TILES: return SDF_E_UNSUPPORTED;   // size is per stream
+    case SDF_FORMAT_SHADE32F: return 16;
     default: return SDF_E_INVALID_ARG;
   }
 }
@@ -732,7 +733,8 @@ int sdf_deinterleave(const void* parts, int32_t nparts, int32_t part_stride_rows
 
 int sdf_heatmap(const int32_t* steps, int32_t count, int32_t which, int32_t max_steps,
                 int32_t format, void* out, void* stream) {
-  if (count < 0 || which < 0 || which > 2 || max_steps < 0 || sdf_format_bytes(format) < 0)
+  if (count < 0 || which < 0 || which > 2 || max_steps < 0 || sdf_format_bytes(format) < 0 ||
+      format == SDF_FORMAT_SHADE32F)   // colours only
     return SDF_E_INVALID_ARG;
   if (count == 0) return SDF_OK;
   if (!steps || !out) return SDF_E_INVALID_ARG;

@@ -1,0 +1,66 @@
+// shade.h -- a pixel's colour from its three shading terms, shared by the
+// render kernels and the TILES decoder (tiles.hip) so that a frame assembled
+// from TILES streams is bit-identical to one rendered in place.
+//
+// voxel_fragment.frag:204-210 (+ the AO extension, DESIGN.md Scene spec):
+//   spec = pow(max(N.H, 0), shininess)            x = max(N.H, 0)
+//   dif  = clamp(N.L, 0, 1) * shadow
+//   c    = la * amb * ao + dif * mat_dif + spec * mat_ref,  alpha 1
+// (ao = 1 without AO: la * amb * 1 is la * amb bit for bit).  The TILES wire
+// carries (ao, dif, x) instead of the colour: the terms are smooth where the
+// colour mixes them, and x^12 spreads x's residuals over 3.6 more bits, so
+// the 4K C4 stream is 29 % smaller (TILES).
+//
+// The operation sequence is pinned here, not left to the translation unit's
+// contraction mode: exact precision is the oracle's unfused fp32 sequence and
+// fp64 pow rounded once (oracle/oracle_core.h shade_pixel), fast precision the
+// FMA chain below.  Units that include this header are built with
+// -ffp-contract=off or =fast-honor-pragmas (sdf3d_amd/build.py), both of
+// which honour the pragma (=fast would fuse across it).
+#pragma once
+
+namespace sdf {
+
+// The frame's shading constants as the kernel uses them (lam = light ambient
+// x material ambient, rounded to fp32 once); TILES stream header words 4..13.
+struct ShadeK {
+  float lam[3], dif[3], ref[3], shin;
+};
+
+// TILES stream header word 2: what the three channels hold
+enum TilesShade : uint32_t {
+  kTilesRaw = 0,         // the channel values themselves (RGB)
+  kTilesShadeFast = 1,   // shading terms of a fast-precision render
+  kTilesShadeExact = 2   // shading terms of an exact-precision render
+};
+
+template <bool EXACT>
+__device__ __forceinline__ float spec_pow(float x, float shin) {
+  if constexpr (EXACT) {
+    return (float)pow((double)x, (double)shin);
+  } else {
+    return __builtin_amdgcn_exp2f(shin * __builtin_amdgcn_logf(x));
+  }
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float shade_channel(float lam, float md, float mr, float ao, float dif,
+                                               float spec) {
+#pragma clang fp contract(off)
+  const float a = lam * ao;
+  if constexpr (EXACT) {
+    return (a + dif * md) + spec * mr;
+  } else {
+    return __builtin_fmaf(spec, mr, __builtin_fmaf(dif, md, a));
+  }
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float4 shade_colour(const ShadeK& K, float ao, float dif, float x) {
+  const float spec = spec_pow<EXACT>(x, K.shin);
+  return make_float4(shade_channel<EXACT>(K.lam[0], K.dif[0], K.ref[0], ao, dif, spec),
+                     shade_channel<EXACT>(K.lam[1], K.dif[1], K.ref[1], ao, dif, spec),
+                     shade_channel<EXACT>(K.lam[2], K.dif[2], K.ref[2], ao, dif, spec), 1.0f);
+}
+
+}  // namespace sdf

@@ -11,7 +11,9 @@
 //               holds the packed rows of its tiling (the interleave
 //               {block_rows, r, nparts}, or any sdf_tiling per part);
 //               every tile is expanded to RGBA32F (alpha 1) straight into its
-//               rows of the assembled frame.  Lane j = pixel (j / 8, j % 8):
+//               rows of the assembled frame; a rendered stream's channels
+//               are the pixels' shading terms, made into the colour here
+//               exactly as the render kernel does (shade.h).  Lane j = pixel (j / 8, j % 8):
 //               the planes arrive by one vector load (lane i: plane i), a
 //               64 x 64 bit transpose gives every lane the concatenation of
 //               its three residuals, then un-zigzag and the tile's 2-D
@@ -25,6 +27,7 @@
 #include <stdint.h>
 
 #include "kernel_args.h"
+#include "shade.h"
 #include "wave_bits.h"
 
 namespace sdf {
@@ -95,6 +98,18 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
   const uint4 hdv = lane < nt ? reinterpret_cast<const uint4*>(base + Lt.head)[tbase + lane]
                               : make_uint4(0u, 0u, 0u, 0u);
   if (present == 0) return;   // no stream: rows rendered in place
+  // what the channels hold, and the frame's shading constants (header words
+  // 2, 4..13: scalar loads)
+  const uint32_t* const hw = reinterpret_cast<const uint32_t*>(base);
+  const uint32_t shade = hw[2];
+  ShadeK K;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    K.lam[c] = __uint_as_float(hw[4 + c]);
+    K.dif[c] = __uint_as_float(hw[7 + c]);
+    K.ref[c] = __uint_as_float(hw[10 + c]);
+  }
+  K.shin = __uint_as_float(hw[13]);
   const uint2* data = reinterpret_cast<const uint2*>(base + Lt.data);
   uint2 pa[TPW];   // lane i: qword i of each tile's data (up to 64)
 #pragma unroll
@@ -231,7 +246,10 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
         ++b;
       }
       const int y = (first_blk + b * period) * brows + w + jb * gap;
-      frame[(size_t)y * width + x] = make_float4(v[0], v[1], v[2], 1.0f);
+      float4 px = make_float4(v[0], v[1], v[2], 1.0f);
+      if (shade == kTilesShadeFast) px = shade_colour<false>(K, v[0], v[1], v[2]);
+      else if (shade == kTilesShadeExact) px = shade_colour<true>(K, v[0], v[1], v[2]);
+      frame[(size_t)y * width + x] = px;
     }
     (void)nq;
   }

@@ -51,6 +51,8 @@ from typing import Callable, Optional
 
 import numpy as np
 
+from . import abi
+
 
 def share_blocks(rank: int, world: int, shares=(1, 1)) -> tuple[int, int, int, int]:
     """(first block, run, period, step) of `rank` in the tiling with shares
@@ -138,7 +140,7 @@ def tiles_data_offset(width: int, rows: int) -> int:
     """Offset of the plane data in a TILES stream of `rows` packed rows
     (include/sdf_abi.h): header, offset table, 16-B heads."""
     n = ((width + 7) // 8) * ((rows + 7) // 8)
-    return (8 + 4 * n + 15) // 16 * 16 + 16 * n
+    return (abi.TILES_HEADER_BYTES + 4 * n + 15) // 16 * 16 + 16 * n
 
 
 class FrameDriver:

@@ -57,7 +57,7 @@ def torch_dtype(fmt: int):
     import torch
     return {abi.FORMAT_RGBA32F: torch.float32, abi.FORMAT_RGBA16F: torch.float16,
             abi.FORMAT_RGBA8: torch.uint8, abi.FORMAT_RGB32F: torch.float32,
-            abi.FORMAT_TILES: torch.uint8}[fmt]
+            abi.FORMAT_TILES: torch.uint8, abi.FORMAT_SHADE32F: torch.float32}[fmt]
 
 
 def tiles_bytes(width: int, rows: int) -> int:
@@ -72,7 +72,7 @@ def tiles_stream_bytes(stream) -> int:
     """Meaningful prefix of a TILES stream on the host: table + used records."""
     import numpy as np
     used, n = np.frombuffer(bytes(stream[:8].cpu().numpy()), dtype=np.uint32)
-    return (8 + 4 * int(n) + 15) // 16 * 16 + 16 * int(n) + int(used)
+    return (abi.TILES_HEADER_BYTES + 4 * int(n) + 15) // 16 * 16 + 16 * int(n) + int(used)
 
 
 def channels(fmt: int) -> int:

@@ -118,8 +118,11 @@ def test_render_rejects_null_output():
                         C.byref(f.material), C.byref(f.params), None, None, None, None)
     assert rc == abi.SDF_E_INVALID_ARG
     assert lib.sdf_deinterleave(None, 1, 1, 1, 1, 8, 0, None, None) == abi.SDF_E_INVALID_ARG
-    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3, 4, 5)] == \
-        [16, 8, 4, 12, abi.SDF_E_UNSUPPORTED, abi.SDF_E_INVALID_ARG]
+    assert [lib.sdf_format_bytes(f) for f in (0, 1, 2, 3, 4, 5, 6)] == \
+        [16, 8, 4, 12, abi.SDF_E_UNSUPPORTED, 16, abi.SDF_E_INVALID_ARG]
+    # the step heat map writes colours: not the shading-term format
+    assert lib.sdf_heatmap(None, 0, 0, 128, abi.FORMAT_SHADE32F, None, None) == \
+        abi.SDF_E_INVALID_ARG
     assert lib.sdf_tiles_decode(None, 1, 0, 8, 8, 8, None, None) == abi.SDF_E_INVALID_ARG
 
 

@@ -6,6 +6,8 @@ the assembled RGBA32F frame.  Lossless is the whole contract, so every test is
 bit-exact: the decoded frame must equal the RGBA32F render byte for byte.
 The format is pinned against the NumPy restatement in tests/tiles_ref.py in
 both directions (GPU stream -> NumPy decoder, NumPy stream -> GPU decoder).
+A rendered stream carries the pixels' shading terms (SDF_FORMAT_SHADE32F),
+from which the decoder makes the colour: bit-identical to the render's own.
 """
 import numpy as np
 import pytest
@@ -50,38 +52,89 @@ def test_tiles_round_trip_bit_exact(renderer, cfg, w, h, pose, prec):
     assert n <= st.numel()
 
 
+def shade_terms(rd, cfg, w, h, pose, prec, t=None):
+    import torch
+    sh, _ = rd.render(frame(cfg, w, h, pose, prec, abi.FORMAT_SHADE32F), t)
+    torch.cuda.synchronize()
+    return sh.cpu().numpy()
+
+
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
 @pytest.mark.parametrize("cfg,w,h,pose", CASES[:4])
-def test_gpu_stream_decodes_with_reference(renderer, cfg, w, h, pose):
+def test_gpu_stream_decodes_with_reference(renderer, cfg, w, h, pose, prec):
     """The stream the kernel writes is the documented layout: byte for byte
-    the NumPy encoder's stream of the same frame, and the NumPy decoder reads
-    it back to the same bits."""
-    ref, st = render_pair(renderer, cfg, w, h, pose, abi.PRECISION_FAST)
+    the NumPy encoder's stream of the frame's shading terms (SHADE32F) with
+    the frame's shading header, and the NumPy decoder reads the terms back to
+    the same bits."""
+    _, st = render_pair(renderer, cfg, w, h, pose, prec)
     s = st.cpu().numpy()
     s = s[:tiles_ref.stream_bytes(s)]
     assert R.tiles_stream_bytes(st) == s.size
-    host = ref.cpu().numpy()
-    e = tiles_ref.encode(host)
+    terms = shade_terms(renderer, cfg, w, h, pose, prec)
+    f = frame(cfg, w, h, pose, prec, abi.FORMAT_TILES)
+    hdr = tiles_ref.shade_header(f.light, f.material, prec == abi.PRECISION_EXACT)
+    e = tiles_ref.encode(terms, hdr)
     n = tiles_ref.tiles_shape(w, h)[0] * tiles_ref.tiles_shape(w, h)[1]
-    table_end, head = 8 + 4 * n, tiles_ref.head_offset(n)
+    table_end, head = tiles_ref.HEADER_BYTES + 4 * n, tiles_ref.head_offset(n)
     assert s.size == e.size
     # every defined field (the alignment gap after the offset table is not)
     assert np.array_equal(s[:table_end], e[:table_end])
     assert np.array_equal(s[head:], e[head:])
-    assert same_bits(tiles_ref.decode(s, w, h), host)
+    assert tiles_ref.header(s)["shade"] == hdr[0]
+    assert same_bits(tiles_ref.decode(s, w, h)[..., :3], terms[..., :3])
 
 
 @pytest.mark.parametrize("cfg,w,h,pose", CASES[:4])
 def test_reference_stream_decodes_on_gpu(renderer, cfg, w, h, pose):
-    """The GPU decoder reads streams written by the NumPy encoder."""
+    """The GPU decoder reads streams written by the NumPy encoder: RGB
+    streams (header mode 0) to their values, shading-term streams to the
+    render's own colours."""
     import torch
     ref, _ = render_pair(renderer, cfg, w, h, pose, abi.PRECISION_FAST)
     host = ref.cpu().numpy()
-    s = tiles_ref.encode(host)
     buf = torch.zeros(tiles_ref.capacity(w, h), dtype=torch.uint8, device=renderer.device)
+    s = tiles_ref.encode(host)
     buf[:s.size] = torch.from_numpy(s).to(renderer.device)
     out = renderer.tiles_decode(buf, 1, buf.numel(), w, h)
     torch.cuda.synchronize()
     assert same_bits(out.cpu().numpy(), host)
+    for prec in (abi.PRECISION_FAST, abi.PRECISION_EXACT):
+        f = frame(cfg, w, h, pose, prec, abi.FORMAT_RGBA32F)
+        want, _ = renderer.render(f)
+        terms = shade_terms(renderer, cfg, w, h, pose, prec)
+        s = tiles_ref.encode(terms, tiles_ref.shade_header(f.light, f.material,
+                                                           prec == abi.PRECISION_EXACT))
+        buf.zero_()
+        buf[:s.size] = torch.from_numpy(s).to(renderer.device)
+        out = renderer.tiles_decode(buf, 1, buf.numel(), w, h)
+        torch.cuda.synchronize()
+        assert same_bits(out.cpu().numpy(), want.cpu().numpy())
+
+
+@pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
+def test_shading_terms_without_ao_or_shadow(renderer, prec):
+    """ao is 1 without AO (the colour's la * amb * 1 is la * amb bit for
+    bit), dif carries no shadow factor without shadows, and the decoded frame
+    still equals the render's."""
+    import torch
+    w, h = 72, 40
+    for flags in (0, abi.FLAG_SHADOW, abi.FLAG_AO):
+        f = frame("C3", w, h, 1, prec, abi.FORMAT_RGBA32F)
+        f.params.flags = flags
+        want, _ = renderer.render(f)
+        fs = f.copy()
+        fs.params.output_format = abi.FORMAT_SHADE32F
+        terms, _ = renderer.render(fs)
+        ft = f.copy()
+        ft.params.output_format = abi.FORMAT_TILES
+        st, _ = renderer.render(ft)
+        out = renderer.tiles_decode(st, 1, st.numel(), w, h)
+        torch.cuda.synchronize()
+        assert same_bits(out.cpu().numpy(), want.cpu().numpy())
+        tm = terms.cpu().numpy()
+        if not flags & abi.FLAG_AO:
+            assert np.all(tm[..., 0] == 1.0)
+        assert np.all(tm[..., 3] == 1.0)
 
 
 def test_special_values_round_trip(renderer):
@@ -138,7 +191,8 @@ def test_steps_unchanged_by_tiles_output(renderer):
 
 def test_compression_on_the_bench_scene(renderer):
     """The point of the format: the 4K CSG frame (C4, here one 8-row band in
-    eight) ships in well under half the bytes of RGB32F."""
+    eight) ships in under a quarter of the bytes of RGB32F (about 2.3 bytes
+    per pixel as shading terms; 3.2 as the colour itself, round 2)."""
     import torch
     w, h = 3840, 2160
     t = R.tiling(3, 8, 8)
@@ -148,7 +202,7 @@ def test_compression_on_the_bench_scene(renderer):
     px = R.owned_rows(h, t) * w
     bpp = R.tiles_stream_bytes(st) / px
     print("C4 TILES bytes/pixel", round(bpp, 3))
-    assert bpp < 6.0
+    assert bpp < 3.0
 
 
 @pytest.mark.parametrize("world,shares", [(2, (1, 2)), (3, (2, 3)), (8, (1, 3))])

@@ -6,12 +6,20 @@ HIP encoder (render_kernel.inc store_tiles + tiles.hip compaction) and decoder
 GPU streams are compared byte for byte with encode() (plane blocks are in tile
 order on both sides) and decoded with decode(); encode() streams feed the GPU
 decoder.  Never on the product path.
+
+A stream's three channels hold RGB (header shade mode 0) or, in a stream
+rendered by sdf_render, the pixels' shading terms (ao, dif, x; mode 1 fast /
+2 exact precision) with the frame's shading constants in the header, from
+which the GPU decoder makes the colour (sdf3d_amd/csrc/shade.h).  This module
+handles the codec: decode() returns the channel values themselves.
 """
 from __future__ import annotations
 
 import numpy as np
 
 MAX_PLANES = 3 * 32
+HEADER_BYTES = 64
+SHADE_RAW, SHADE_FAST, SHADE_EXACT = 0, 1, 2
 
 
 def tiles_shape(width: int, rows: int) -> tuple[int, int]:
@@ -19,7 +27,7 @@ def tiles_shape(width: int, rows: int) -> tuple[int, int]:
 
 
 def head_offset(ntiles: int) -> int:
-    return (8 + 4 * ntiles + 15) // 16 * 16
+    return (HEADER_BYTES + 4 * ntiles + 15) // 16 * 16
 
 
 def data_offset(ntiles: int) -> int:
@@ -93,8 +101,28 @@ def _pack_fields(fields) -> bytes:
     return acc.to_bytes(8 * nq, "little")
 
 
-def encode(rgb: np.ndarray) -> np.ndarray:
-    """[rows, width, >=3] float32 -> uint8 stream."""
+def shade_header(light, material, precision_exact: bool) -> tuple[int, np.ndarray]:
+    """(mode, 10 float32 shading constants) a render of this light and
+    material writes into its stream header: light.ambient * material.amb[c]
+    rounded to fp32, material.dif, material.ref, shininess."""
+    la = np.float32(light.ambient)
+    k = [np.float32(la * np.float32(material.amb[c])) for c in range(3)]
+    k += [np.float32(material.dif[c]) for c in range(3)]
+    k += [np.float32(material.ref[c]) for c in range(3)]
+    k.append(np.float32(material.shininess))
+    return (SHADE_EXACT if precision_exact else SHADE_FAST), np.array(k, dtype=np.float32)
+
+
+def header(stream: np.ndarray) -> dict:
+    """The stream header's fields."""
+    w = np.frombuffer(np.asarray(stream[:HEADER_BYTES], dtype=np.uint8).tobytes(), dtype=np.uint32)
+    return {"used": int(w[0]), "ntiles": int(w[1]), "shade": int(w[2]),
+            "k": w[4:14].view(np.float32).copy()}
+
+
+def encode(rgb: np.ndarray, shade: tuple[int, np.ndarray] | None = None) -> np.ndarray:
+    """[rows, width, >=3] float32 -> uint8 stream; `shade` = (mode, constants)
+    for a stream of shading terms (shade_header), None for RGB."""
     rows, width = rgb.shape[:2]
     ty, tx = tiles_shape(width, rows)
     n = ty * tx
@@ -148,22 +176,28 @@ def encode(rgb: np.ndarray) -> np.ndarray:
         blocks.append(data)
         off += len(data)
     out = np.zeros(data_offset(n) + off, dtype=np.uint8)
-    out[:8] = np.frombuffer(np.array([off, n], dtype=np.uint32).tobytes(), dtype=np.uint8)
-    out[8:8 + 4 * n] = np.frombuffer(table.tobytes(), dtype=np.uint8)
+    hw = np.zeros(HEADER_BYTES // 4, dtype=np.uint32)
+    hw[0], hw[1] = off, n
+    if shade is not None:
+        hw[2] = shade[0]
+        hw[4:14] = np.asarray(shade[1], dtype=np.float32).view(np.uint32)
+    out[:HEADER_BYTES] = np.frombuffer(hw.tobytes(), dtype=np.uint8)
+    out[HEADER_BYTES:HEADER_BYTES + 4 * n] = np.frombuffer(table.tobytes(), dtype=np.uint8)
     out[head_offset(n):data_offset(n)] = np.frombuffer(heads.tobytes(), dtype=np.uint8)
     out[data_offset(n):] = np.frombuffer(b"".join(blocks), dtype=np.uint8)
     return out
 
 
 def decode(stream: np.ndarray, width: int, rows: int) -> np.ndarray:
-    """uint8 stream -> [rows, width, 4] float32, alpha = 1."""
+    """uint8 stream -> [rows, width, 4] float32: the three channel values
+    (RGB, or the shading terms of a rendered stream), alpha = 1."""
     s = np.asarray(stream, dtype=np.uint8)
     ty, tx = tiles_shape(width, rows)
     n = ty * tx
     used, ntiles = np.frombuffer(s[:8].tobytes(), dtype=np.uint32)
     if ntiles != n:
         raise ValueError(f"stream has {ntiles} tiles, expected {n}")
-    table = np.frombuffer(s[8:8 + 4 * n].tobytes(), dtype=np.uint32)
+    table = np.frombuffer(s[HEADER_BYTES:HEADER_BYTES + 4 * n].tobytes(), dtype=np.uint32)
     heads = np.frombuffer(s[head_offset(n):data_offset(n)].tobytes(), dtype=np.uint32).reshape(n, 4)
     base = data_offset(n)
     out = np.ones((ty * 8, tx * 8, 4), dtype=np.float32)

@@ -37,7 +37,7 @@ def main():
     for spec in a.libs:
         name, path = spec.split("=", 1)
         rd = Renderer("cuda:0")
-        rd.lib = abi.load_library(path)
+        rd.lib = abi.load_library(path, any_version=True)
         rds[name] = rd
     prec = abi.PRECISION_FAST if a.precision == "fast" else abi.PRECISION_EXACT
     res = {}

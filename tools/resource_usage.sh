@@ -3,7 +3,7 @@
 # kernel-resource-usage remarks:  tools/resource_usage.sh [grep pattern]
 #   one line per kernel: name  SGPRs  VGPRs  scratch  waves/SIMD
 root=$(cd "$(dirname "$0")/.." && pwd)
-/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=fast -fno-slp-vectorize \
+/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=fast-honor-pragmas -fno-slp-vectorize \
   -I "$root/sdf3d_amd/build" -c "$root/sdf3d_amd/csrc/render_fast.hip" -o /tmp/_ru.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 |
   sed -n -e 's/.*remark: *//' -e 's/ \[-Rpass.*//p' |

@@ -43,7 +43,7 @@ def main():
     from sdf3d_amd import Renderer, abi, renderer as R, scenes
     rd = Renderer("cuda:0")
     if args.lib:
-        rd.lib = abi.load_library(args.lib)
+        rd.lib = abi.load_library(args.lib, any_version=True)
     N, K = args.world, args.frames
     f = scenes.config(args.config, precision=abi.PRECISION_FAST)
     W, H = f.params.width, f.params.height
