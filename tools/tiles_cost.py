@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--n", type=int, default=50)
     ap.add_argument("--whole-only", action="store_true")
+    ap.add_argument("--share", default=None,
+                    help="WORLD:A:B -- time only rank 1's share of that tiling (e.g. 8:2:7)")
     args = ap.parse_args()
     import torch
     from sdf3d_amd import Renderer, abi, renderer as R, scenes
@@ -48,7 +50,10 @@ def main():
     for name, t in [("whole", None), ("half_of_2", R.tiling(1, 2, 8)),
                     ("share_3_of_7_N2", R.tiling(1, 2, 8, shares=(4, 3))),
                     ("quarter_of_4", R.tiling(1, 4, 8)),
-                    ("share_2_of_15_N8", R.tiling(1, 8, 8, shares=(1, 2)))][:1 if args.whole_only else 5]:
+                    ("share_2_of_15_N8", R.tiling(1, 8, 8, shares=(1, 2)))][:1 if args.whole_only else 5] \
+            if not args.share else \
+            [(f"share_{args.share}", R.tiling(1, int(args.share.split(":")[0]), 8,
+                                              shares=tuple(int(v) for v in args.share.split(":")[1:])))]:
         p, q = timed(plain, t, args.n), timed(tiles, t, args.n)
         out[name] = {"rgba32f_ms": p, "tiles_ms": q, "overhead": round(q / p - 1, 4)}
         if t is None:
