@@ -13,6 +13,8 @@ frame period at N is bounded below by max(root, peer):
     root_both      both, decode on the side stream as the frame driver does
     root_serial    both on one stream (no overlap)
     peer_tiles     one peer's share as TILES, frames on 3 streams
+    peer_plain     the same share as plain RGBA32F (the TILES wire's cost is
+                   peer_tiles - peer_plain)
 
     python tools/root_probe.py [--world 8] [--shares 1:3] [--config C4] [--frames 200]
 """
@@ -36,7 +38,7 @@ def main():
     ap.add_argument("--shares", default="1:1", help="rank 0 : other ranks, blocks per period")
     ap.add_argument("--streams", type=int, default=3, help="alternating streams / buffers")
     ap.add_argument("--lib", default=None, help="another libsdf3d.so build (A/B)")
-    ap.add_argument("--only", choices=["decode", "root", "peer"], default=None,
+    ap.add_argument("--only", choices=["decode", "root", "peer", "peer_plain"], default=None,
                     help="time one leg only (for rocprofv3 counter passes)")
     args = ap.parse_args()
     import torch
@@ -63,11 +65,15 @@ def main():
     # the busiest peer: the most rows
     busiest = max(range(1, N), key=lambda r: R.owned_rows(H, tilings[r])) if N > 1 else 0
     peer_bufs = [torch.empty(stride, dtype=torch.uint8, device=rd.device) for _ in range(NS)]
+    prow = R.owned_rows(H, tilings[busiest])
+    peer_plain = [torch.empty((prow, W, 4), dtype=torch.float32, device=rd.device) for _ in range(NS)]
 
-    def run(render=True, decode=True, serial=False, peer=False):
+    def run(render=True, decode=True, serial=False, peer=False, plain=False):
+        pf = f if plain else ft
         for b in range(NS):
             if peer:
-                rd.render(ft, tilings[busiest], out=peer_bufs[b], stream=streams[b])
+                rd.render(pf, tilings[busiest], out=peer_plain[b] if plain else peer_bufs[b],
+                          stream=streams[b])
             if render:
                 rd.render(f, t0_tiling, out=frames[b], stream=streams[b])
             if decode:
@@ -79,7 +85,8 @@ def main():
             b = i % NS
             s = streams[b]
             if peer:
-                rd.render(ft, tilings[busiest], out=peer_bufs[b], stream=s)
+                rd.render(pf, tilings[busiest], out=peer_plain[b] if plain else peer_bufs[b],
+                          stream=s)
                 continue
             if render:
                 rd.render(f, t0_tiling, out=frames[b], stream=s)
@@ -102,8 +109,10 @@ def main():
     out = {"config": args.config, "world": N, "shares": args.shares, "frames": K, "streams": NS}
     if args.only:
         leg = {"decode": dict(render=False), "root": dict(), "peer": dict(render=False,
-               decode=False, peer=True)}[args.only]
-        out[args.only + "_ms"] = run(**leg)
+               decode=False, peer=True),
+               "peer_plain": dict(render=False, decode=False, peer=True, plain=True)}[args.only]
+        for _ in range(2):   # the second pass (warm clocks) is the reported one
+            out[args.only + "_ms"] = run(**leg)
         print(json.dumps(out))
         return
     out["frame_fill_ms"] = fill()   # the write floor of one RGBA32F frame
@@ -113,6 +122,7 @@ def main():
         out["root_both_ms"] = run()
         out["root_serial_ms"] = run(serial=True)
         out["peer_tiles_ms"] = run(render=False, decode=False, peer=True)
+        out["peer_plain_ms"] = run(render=False, decode=False, peer=True, plain=True)
     print(json.dumps(out, indent=1))
 
 
