@@ -150,7 +150,7 @@ int make_context(const std::vector<int>& devs, int W, int H, int a, int b,
 // sdf3d_amd/multigpu.py choose_shares): rank 0 also decodes everyone's streams.
 void default_shares(int n, int* a, int* b) {
   static const int kShares[9][2] = {{1, 1}, {1, 1}, {1, 1}, {1, 1}, {3, 4},
-                                    {3, 4}, {1, 2}, {1, 2}, {1, 3}};
+                                    {3, 4}, {1, 2}, {1, 2}, {2, 7}};
   const int k = n < 9 ? n : 8;
   *a = kShares[k][0];
   *b = kShares[k][1];

@@ -96,6 +96,15 @@ def owned_rows_py(height: int, rank: int, world: int, block_rows: int = 8,
 FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.444, "decode": 0.043, "floor": 0.026,
                   "wire": 0.41}
 
+# Shares measured best on one MI355X with rank 0's and the busiest peer's
+# per-frame GPU work (tools/root_probe.py, 4 streams, shading-term TILES;
+# profiles/r03_share_probe_C4.json), max(rank 0, peer) ms per frame:
+#   N = 2: 1:1 0.188, 4:3 0.204, 3:2 0.212
+#   N = 4: 3:4 0.102, 4:5 0.103, 2:3 0.105, 1:1 0.112
+#   N = 8: 2:7 0.0532, 1:4 0.0538, 1:3 0.0548
+# The cost model below serves the other world sizes (and explicit costs).
+MEASURED_SHARES = {2: (1, 1), 4: (3, 4), 8: (2, 7)}
+
 
 def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int]:
     """Shares (a, b) for the TILES frame driver: rank 0 renders its rows in
@@ -107,9 +116,11 @@ def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int
     N = 8 (rank 0 / busiest peer GPU work, ms per frame, escape-coded TILES):
     1:2 0.064 / 0.057, 1:3 0.058 / 0.060, 1:4 0.055 / 0.061, 2:7 0.055 /
     0.062 (profiles/r01_root_probe_C4.json)."""
-    c = costs or FRAME_COSTS_MS
     if world <= 1:
         return (1, 1)
+    if costs is None and world in MEASURED_SHARES:
+        return MEASURED_SHARES[world]
+    c = costs or FRAME_COSTS_MS
     best = None
     for period_first in range(2, 2 * max_blocks + 1):
         for a in range(1, max_blocks + 1):

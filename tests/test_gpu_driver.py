@@ -142,7 +142,7 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
     place, and one FIFO engine per rank makes any cross-communicator order
     mismatch between ranks an error.  Rank 0's assembled last frame must equal a single-device
     render bit for bit; the 8-rank C4 case is the round-end N = 8 bench's
-    configuration (4K, default 1:3 shares)."""
+    configuration (4K, default 2:7 shares)."""
     import json
     import subprocess
     import sys
@@ -163,7 +163,7 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
     assert d["config"]["driver"].startswith("native"), d["config"]
     assert d["config"]["wire"] == "tiles"
     if nproc == 8:
-        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 1 / others 3")
+        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 2 / others 7")
 
 
 def _read_ppm(path):
