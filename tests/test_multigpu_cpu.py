@@ -142,6 +142,15 @@ def test_choose_shares():
     assert a < b                            # rank 0 decodes 7 streams: fewer rows
     # with a free decode the shares balance renders alone
     assert choose_shares(8, {"render": 1.0, "render_tiles": 1.0, "decode": 0.0}) == (1, 1)
+    # the measured defaults (tools/root_probe.py, profiles/r03_share_probe_C4.json)
+    assert [choose_shares(w) for w in (2, 4, 8)] == [(1, 1), (3, 4), (2, 7)]
+    # every default tiling covers the frame exactly once
+    for w in range(2, 9):
+        a, b = choose_shares(w)
+        seen = np.zeros(2160, dtype=int)
+        for r in range(w):
+            seen[owned_row_ids(2160, r, w, shares=(a, b))] += 1
+        assert (seen == 1).all()
 
 
 @pytest.mark.parametrize("H", [1, 8, 43, 600, 2160])
