@@ -587,6 +587,8 @@ def test_culling_exact_on_random_scenes(renderer, seed):
     ((4.0, 2.0, -3.0), 60.0),     # hard k
     ((0.0, 0.3, -0.1), 10.0),     # light inside the cluster sphere
     ((3.0, -1.0, 0.0), 10.0),     # light below the plane: b < 0
+    ((4.0, 2.0, -3.0), 0.05),     # tiny k: terms far below s (the exact march's
+    ((4.0, 2.0, -3.0), 1.0e4),    # division skip never / almost always applies)
 ])
 @pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
 def test_shadow_lit_tail_exact(renderer, light, k, prec):
