@@ -8,7 +8,6 @@ GPU: its frames must equal a one-device sdf_render bit for bit.
 RCCL refuses two ranks on one GPU, so the multi-rank collective order is
 pinned by the gloo rehearsal of the same sequence (test_multigpu_cpu.py)."""
 import os
-import socket
 
 import pytest
 import torch
@@ -17,9 +16,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from netutil import free_port
+    return free_port()
 
 
 @pytest.fixture(scope="module")
@@ -144,19 +142,20 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
     render bit for bit; the 8-rank C4 case is the round-end N = 8 bench's
     configuration (4K, default 2:7 shares)."""
     import json
-    import subprocess
     import sys
     assert SHMCOMM.exists(), "build() must produce tests/shmcomm/libshmcomm.so"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "6", "--warmup", "2",
-           "--backend", "gloo", "--comm-lib", str(SHMCOMM), "--driver", "native",
-           "--config", cfg, "--no-display", "--clock-warm-s", "0"]
-    if shares:
-        cmd += ["--shares", shares]
+    from netutil import run_launcher
+
+    def cmd(port):
+        c = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+             str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
+             str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "6", "--warmup", "2",
+             "--backend", "gloo", "--comm-lib", str(SHMCOMM), "--driver", "native",
+             "--config", cfg, "--no-display", "--clock-warm-s", "0"]
+        return c + (["--shares", shares] if shares else [])
     env = dict(os.environ, SHMCOMM_TIMEOUT_MS="60000", GPU_MAX_HW_QUEUES="8",
                    SHMCOMM_REQUIRE_ASYNC="1")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    r = run_launcher(cmd, timeout=400, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == nproc and d["frame_verified"] is True, d

@@ -435,20 +435,17 @@ def test_multirank_bench_rehearsal(renderer, tmp_path, nproc, wire, shares):
     0, unequal row shares) or the RGB32F wire (sdf_deinterleave) --
     assembles frames bit-identical to a single-device render."""
     import json
-    import socket
-    import subprocess
     import sys
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    from netutil import run_launcher
     root = Path(__file__).resolve().parent.parent
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-           str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
-           str(root / "bench.py"), "--gpus", str(nproc), "--steps", "4", "--warmup", "2",
-           "--backend", "gloo", "--config", "C3", "--wire", wire, "--no-display"]
-    if shares:
-        cmd += ["--shares", shares]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+
+    def cmd(port):
+        c = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+             str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
+             str(root / "bench.py"), "--gpus", str(nproc), "--steps", "4", "--warmup", "2",
+             "--backend", "gloo", "--config", "C3", "--wire", wire, "--no-display"]
+        return c + (["--shares", shares] if shares else [])
+    r = run_launcher(cmd, timeout=300, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)

@@ -3,7 +3,6 @@ the gloo backend (world size 2 and 3) and a CPU stand-in for the render
 kernel (the oracle) and for sdf_deinterleave.  Rank 0's assembled frames
 must equal whole-frame renders bit for bit (pixels are independent)."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -19,9 +18,8 @@ from sdf3d_amd.multigpu import (FrameDriver, deinterleave_index, deinterleave_to
 
 
 def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from netutil import free_port as pick
+    return pick()
 
 
 def frame_for(step):
