@@ -34,9 +34,36 @@ enum TilesShade : uint32_t {
   kTilesShadeExact = 2   // shading terms of an exact-precision render
 };
 
+// Exact precision: pow in fp64, rounded to fp32 once (the oracle's cr_powf).
+// For an integer exponent n in [0, 64] (the shininess, a uniform; 12 by
+// default) x^n by repeated squaring in fp64 instead of the library pow (~130
+// fp64 instructions): x^2 is exact (48-bit product) and each further product
+// adds at most 2^-53 relative, so the value lies within n 2^-53 < 2^-46 of
+// x^n.  Where both ends of a 2^-44 interval around it round to the same
+// float, that float is the correct rounding of x^n -- and of the library's
+// fp64 pow, which lies in the same interval; other lanes (rounding
+// boundaries, NaN) take the library pow.
 template <bool EXACT>
 __device__ __forceinline__ float spec_pow(float x, float shin) {
+#pragma clang fp contract(off)
   if constexpr (EXACT) {
+    const int n = (int)shin;
+    if ((float)n == shin && n >= 0 && n <= 64) {
+      double b = (double)x, v = 1.0;
+      for (int e = n; e != 0; e >>= 1) {
+        if (e & 1) v = v * b;
+        if (e > 1) b = b * b;
+      }
+      const double tol = 0x1p-44 * __builtin_fabs(v);
+      const float r = (float)v;
+      const bool ok = ((float)(v - tol) == r) & ((float)(v + tol) == r);
+      float out = r;
+      if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        asm volatile("" ::: "memory");   // keep the library pow out of the fast path
+        out = ok ? r : (float)pow((double)x, (double)shin);
+      }
+      return out;
+    }
     return (float)pow((double)x, (double)shin);
   } else {
     return __builtin_amdgcn_exp2f(shin * __builtin_amdgcn_logf(x));
