@@ -54,6 +54,10 @@ def load(variant: str = "ieee") -> C.CDLL:
     lib.sdf_oracle_replay.argtypes = frame_args + [P(abi.sdf_tiling), C.c_void_p, C.c_void_p,
                                                    C.c_void_p, C.c_int]
     lib.sdf_oracle_replay.restype = C.c_int
+    if hasattr(lib, "sdf_oracle_render_terms"):
+        lib.sdf_oracle_render_terms.argtypes = frame_args + [P(abi.sdf_tiling), C.c_void_p,
+                                                             C.c_int]
+        lib.sdf_oracle_render_terms.restype = C.c_int
     lib.sdf_oracle_owned_rows.argtypes = [C.c_int, P(abi.sdf_tiling)]
     lib.sdf_oracle_owned_rows.restype = C.c_int
     lib.sdf_oracle_scene_sdf.argtypes = [P(abi.sdf_scene), C.c_float, C.c_float, C.c_float]
@@ -147,6 +151,41 @@ def render(frame, t=None, nthreads: int | None = None, twin: bool = False,
     if rc != 0:
         raise RuntimeError(f"oracle render failed: {rc}")
     return rgba, steps
+
+
+def render_terms(frame, t=None, nthreads: int | None = None, variant: str = "ieee"):
+    """Each pixel's shading terms (ao, dif, max(N.H, 0), 1) of the fp32
+    restatement instead of its colour: the reference of SDF_FORMAT_SHADE32F
+    (what the TILES wire carries).  Returns float32 [rows, W, 4]."""
+    lib = load(variant)
+    p = frame.params
+    rows = owned_rows(p.height, t)
+    out = np.empty((rows, p.width, 4), dtype=np.float32)
+    rc = lib.sdf_oracle_render_terms(C.byref(frame.scene), C.byref(frame.camera),
+                                     C.byref(frame.light), C.byref(frame.material),
+                                     C.byref(frame.params), C.byref(t) if t is not None else None,
+                                     out.ctypes.data_as(C.c_void_p),
+                                     nthreads if nthreads is not None else default_threads())
+    if rc != 0:
+        raise RuntimeError(f"oracle render_terms failed: {rc}")
+    return out
+
+
+def colour_from_terms(frame, terms):
+    """The colour from the terms in the restatement's own operation order
+    (oracle_core.h shade_pixel, voxel_fragment.frag:204-210): fp32 products
+    and sums, pow in fp64 rounded once.  [.., 4] float32 -> [.., 4] float32."""
+    f32 = np.float32
+    m, li = frame.material, frame.light
+    ao, dif, x = (terms[..., i].astype(f32) for i in range(3))
+    with np.errstate(all="ignore"):
+        spec = np.power(x.astype(np.float64), np.float64(f32(m.shininess))).astype(f32)
+        out = np.empty(terms.shape, dtype=f32)
+        for c in range(3):
+            amb = f32(f32(li.ambient) * f32(m.amb[c]))
+            out[..., c] = (f32(amb) * ao + dif * f32(m.dif[c])) + spec * f32(m.ref[c])
+    out[..., 3] = 1.0
+    return out
 
 
 def replay(frame, steps, t=None, mask=None, nthreads: int | None = None, variant: str = "ieee"):

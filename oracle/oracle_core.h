@@ -395,6 +395,9 @@ static void FN(render_rows)(const sdf_scene* s, const sdf_light* li,
       FN(v3) cam = FN(mk)(u->cam[0], u->cam[1], u->cam[2]);
       size_t o = (size_t)pr * W + x;
       FN(shade_pixel)(s, li, M, pa, cam, ray, rgba + 4 * o, steps ? steps + 2 * o : 0, fo);
+#ifdef ORACLE_PIXEL_OUT_HOOK
+      ORACLE_PIXEL_OUT_HOOK(rgba + 4 * o);   /* sdf_oracle_render_terms only */
+#endif
     }
   }
 }

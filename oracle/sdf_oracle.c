@@ -40,6 +40,26 @@ typedef struct {
  * it links (the exact-precision kernel evaluates them the same way). */
 static inline float cr_logf(float x) { return (float)log((double)x); }
 static inline float cr_powf(float x, float y) { return (float)pow((double)x, (double)y); }
+/* sdf_oracle_render_terms (below): each pixel's shading terms (ao, dif,
+ * max(N.H, 0), 1) -- what SDF_FORMAT_SHADE32F and the TILES wire carry --
+ * recorded by the restatement's instrumentation hook and written instead of
+ * the colour while g_terms_out is set (one render at a time).  Tools that
+ * define their own hook (tools/terms_probe.c) leave these out. */
+#ifndef ORACLE_TERMS_HOOK
+static _Thread_local float t_terms[3];
+static int g_terms_out;
+#define ORACLE_TERMS_HOOK(ao, dif, spec, x, ndl, sh) \
+  (t_terms[0] = (float)(ao), t_terms[1] = (float)(dif), t_terms[2] = (float)(x))
+#define ORACLE_PIXEL_OUT_HOOK(px)                                               \
+  do {                                                                          \
+    if (g_terms_out) {                                                          \
+      (px)[0] = t_terms[0]; (px)[1] = t_terms[1]; (px)[2] = t_terms[2];          \
+      (px)[3] = 1.0f;                                                           \
+    }                                                                           \
+  } while (0)
+#define ORACLE_HAVE_TERMS 1
+#endif
+
 #define REAL float
 #define FN(name) f32_##name
 #define SQRT sqrtf
@@ -236,6 +256,19 @@ int sdf_oracle_render_f64(const sdf_scene* s, const sdf_camera* c, const sdf_lig
                           float* rgba, int* steps, int nthreads) {
   return render(1, s, c, l, m, p, t, rgba, steps, 0, nthreads);
 }
+
+#ifdef ORACLE_HAVE_TERMS
+/* The fp32 restatement's shading terms per pixel instead of its colour
+ * (test infrastructure: the SHADE32F / TILES terms' reference). */
+int sdf_oracle_render_terms(const sdf_scene* s, const sdf_camera* c, const sdf_light* l,
+                            const sdf_material* m, const sdf_params* p, const sdf_tiling* t,
+                            float* rgba, int nthreads) {
+  g_terms_out = 1;
+  const int rc = render(0, s, c, l, m, p, t, rgba, 0, 0, nthreads);
+  g_terms_out = 0;
+  return rc;
+}
+#endif
 
 /* Forced-step replay: the fp32 restatement with each pixel's primary and
  * shadow marches run for exactly force[2i], force[2i+1] iterations (capped

@@ -111,6 +111,18 @@ def test_reference_stream_decodes_on_gpu(renderer, cfg, w, h, pose):
         assert same_bits(out.cpu().numpy(), want.cpu().numpy())
 
 
+@pytest.mark.parametrize("cfg,w,h,pose", CASES)
+def test_exact_terms_equal_oracle_terms(renderer, cfg, w, h, pose):
+    """SDF_FORMAT_SHADE32F in exact precision is the oracle's own terms bit
+    for bit (oracle.render_terms; their colour is the oracle's colour,
+    tests/test_terms.py)."""
+    import oracle
+    terms = shade_terms(renderer, cfg, w, h, pose, abi.PRECISION_EXACT)
+    f = frame(cfg, w, h, pose, abi.PRECISION_EXACT, abi.FORMAT_SHADE32F)
+    ref = oracle.render_terms(f)
+    assert same_bits(terms, ref)
+
+
 @pytest.mark.parametrize("prec", [abi.PRECISION_EXACT, abi.PRECISION_FAST])
 def test_shading_terms_without_ao_or_shadow(renderer, prec):
     """ao is 1 without AO (the colour's la * amb * 1 is la * amb bit for
