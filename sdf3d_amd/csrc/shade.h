@@ -42,11 +42,15 @@ enum TilesShade : uint32_t {
 // x^n.  Where both ends of a 2^-44 interval around it round to the same
 // float, that float is the correct rounding of x^n -- and of the library's
 // fp64 pow, which lies in the same interval; other lanes (rounding
-// boundaries, NaN) take the library pow.
+// boundaries, NaN) take the library pow.  SDF_SHADE_LIBRARY_POW (the TILES
+// decoder, tiles.hip): the library pow alone -- the same floats; there its
+// code size keeps the decoder's tile loop rolled at 8 waves/SIMD, which
+// decodes fast-precision streams 2 % faster than the unrolled loop at 7.
 template <bool EXACT>
 __device__ __forceinline__ float spec_pow(float x, float shin) {
 #pragma clang fp contract(off)
   if constexpr (EXACT) {
+#ifndef SDF_SHADE_LIBRARY_POW
     const int n = (int)shin;
     if ((float)n == shin && n >= 0 && n <= 64) {
       double b = (double)x, v = 1.0;
@@ -64,6 +68,7 @@ __device__ __forceinline__ float spec_pow(float x, float shin) {
       }
       return out;
     }
+#endif
     return (float)pow((double)x, (double)shin);
   } else {
     return __builtin_amdgcn_exp2f(shin * __builtin_amdgcn_logf(x));

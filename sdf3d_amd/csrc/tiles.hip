@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include "kernel_args.h"
+#define SDF_SHADE_LIBRARY_POW 1   // see shade.h spec_pow
 #include "shade.h"
 #include "wave_bits.h"
 
