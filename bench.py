@@ -189,7 +189,7 @@ def roofline(pmc, alg_flops, kavg_ms, store_bytes):
     half-rate min/max/cmp as one unit, so it is a lower bound (a v_min-only
     chain reads 0.60).  alg_equiv is the SURVEY.md 8(d) counting rule (every
     primitive at every step, oracle step counts): exact culling skips
-    evaluations that rule counts, so it can exceed the peak."""
+    evaluations that rule counts, so its `survey_rule_ratio` can exceed 1."""
     roof = {"bound": "valu", "achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": None, "traffic": pmc.get("hbm_bytes_per_launch"),
             "kernel_ms": round(kavg_ms, 4),
@@ -210,13 +210,48 @@ def roofline(pmc, alg_flops, kavg_ms, store_bytes):
                                   / (1024 * c["GRBM_GUI_ACTIVE"] / 8), 4)
     if alg_flops is not None:
         alg = alg_flops / (kavg_ms * 1e-3) / 1e12
+        # not a roofline fraction: the rule counts evaluations the exact
+        # culling never performs, so this ratio may exceed 1
         roof["alg_equiv"] = {"flops_per_launch": alg_flops, "TFLOPs": round(alg, 2),
-                             "frac": round(alg / FP32_PEAK_TFLOPS, 4),
-                             "note": "SURVEY 8(d) rule: every primitive at every step; "
-                                     "exact culling skips evaluations it counts"}
+                             "survey_rule_ratio": round(alg / FP32_PEAK_TFLOPS, 4),
+                             "note": "SURVEY 8(d) rule (every primitive at every step, oracle "
+                                     "step counts) over the live kernel time, / 157.3 TF; exact "
+                                     "culling skips evaluations it counts, so it may exceed 1 "
+                                     "and is no roofline fraction"}
     if roof["achieved"] is None and alg_flops is None:
         return None
     return roof
+
+
+def parity_summary(cfg, precision):
+    """What the timed kernel satisfies: the committed full-size parity result
+    of this configuration and precision (profiles/parity_fullsize.json,
+    written by tests/test_gpu_parity.py test_full_size_pixel_parity on the
+    GPU: the frame against a live oracle render, per pixel, outliers
+    diagnosed by the forced-step replay), applied only to a library whose
+    sdf_kernel_id matches the one it was taken from."""
+    from sdf3d_amd import abi
+    p = ROOT / "profiles" / "parity_fullsize.json"
+    try:
+        rec = json.loads(p.read_text()).get(f"{cfg}/{precision}")
+    except Exception:
+        rec = None
+    if rec is None:
+        return {"source": None, "note": f"no full-size parity result for {cfg}/{precision}"}
+    prec = abi.PRECISION_FAST if precision == "fast" else abi.PRECISION_EXACT
+    kid = abi.load_library().sdf_kernel_id(prec)
+    kid = kid.decode() if kid else None
+    out = {"precision": precision, "policy": rec.get("policy"), "pixels": rec.get("pixels"),
+           "bit_exact": rec.get("bit_exact"), "outliers_over_1e-4": rec.get("outliers"),
+           "replay_diagnosed": rec.get("replay_diagnosed"),
+           "undiagnosed": rec.get("undiagnosed"), "over_0.05": rec.get("over_max_err"),
+           "max_err": rec.get("max_err"), "undiagnosed_max_err": rec.get("undiagnosed_max_err"),
+           "strict_policy_met": rec.get("policy") == "strict",
+           "within_1e-4_everywhere": rec.get("outliers") == 0,
+           "kernel_id": rec.get("kernel_id"), "source": f"profiles/{p.name}"}
+    if rec.get("kernel_id") != kid:
+        out["stale"] = (f"taken from kernel build {rec.get('kernel_id')}, the library's is {kid}")
+    return out
 
 
 def lib_bpp(frame):
@@ -499,7 +534,8 @@ def main():
                  "ms_per_step": round(el_e / args.steps * 1e3, 4),
                  "kernel_ms": round(kavg_e, 4),
                  "roofline": roofline(pmc_e, rank_flops(fe, t, args.pose), kavg_e,
-                                      rows * W * lib_bpp(frame))}
+                                      rows * W * lib_bpp(frame)),
+                 "parity": parity_summary(args.config, "exact")}
 
     # the same frames without the gather (scaling with and
     # without it): each rank renders its blocks only, max over ranks
@@ -583,6 +619,8 @@ def main():
         pmc = (pmc_summary(args.config, args.precision)
                if world == 1 and args.format == "rgba32f" else {})
         out["roofline"] = roofline(pmc, flops, kavg_ms, rows * W * lib_bpp(frame))
+        # the full-size parity of the precision `value` was timed in
+        out["parity"] = parity_summary(args.config, args.precision)
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline ...")
             out["cpu_baseline"] = cpu_baseline(frame, args.cpu_sample_stride, args.cpu_frames)

@@ -19,8 +19,8 @@ import pytest
 
 import oracle
 from golden.make_golden import FIXTURES, frame_for
-from parity import (assert_parity, assert_parity_frame, compare, full_size_conditioning,
-                    quantize, reading_spread, report)
+from parity import (assert_parity, assert_parity_frame, assert_regression, compare,
+                    full_size_conditioning, quantize, reading_spread, report)
 from sdf3d_amd import abi, renderer as R, scenes
 
 pytestmark = pytest.mark.gpu
@@ -318,10 +318,16 @@ def test_full_size_pixel_parity(renderer, cfg, prec):
     px_equal = float(np.mean(np.all(st == ref_st, axis=-1)))
     rep = check_frame(f"fullsize_pixels/{cfg}/{'exact' if prec == 0 else 'fast'}", f, rgba, st,
                       ref, ref_st)
+    kid = abi.load_library().sdf_kernel_id(prec)
     rep.update(width=W, height=H, steps_equal_frac=px_equal, oracle_s=round(t_oracle, 2),
-               path="steps=None (bench path, shadow skip active)")
+               path="steps=None (bench path, shadow skip active)", config=cfg,
+               precision="exact" if prec == 0 else "fast",
+               kernel_id=kid.decode() if kid else None)
     if prec == abi.PRECISION_EXACT:
         assert px_equal == 1.0
+    else:
+        # the kernel's own last full-size measurement (tests/golden/fast_regression.json)
+        assert_regression(rep, f"{cfg}_p0", what=f"fullsize_pixels/{cfg}/fast")
 
 
 def test_invalid_arguments_are_rejected_on_device(renderer):
@@ -395,6 +401,12 @@ def test_write_results():
     out = Path("gpurun_out")
     out.mkdir(exist_ok=True)
     (out / "parity_results.json").write_text(json.dumps(RESULTS, indent=1, sort_keys=True))
+    # the full-size frames alone, keyed "<cfg>/<precision>" with the kernel_id
+    # they were taken from: bench.py's `parity` object reads the committed
+    # copy (profiles/parity_fullsize.json)
+    full = {k.split("/", 1)[1]: v for k, v in RESULTS.items() if k.startswith("fullsize_pixels/")}
+    if full:
+        (out / "parity_fullsize.json").write_text(json.dumps(full, indent=1, sort_keys=True))
 
 
 def read_ppm(path):

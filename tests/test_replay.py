@@ -174,3 +174,47 @@ def test_conditioning_fixture_reproduces_c2():
     from make_conditioning import measure
     want = json.loads((here / "conditioning.json").read_text())["C2_p1"]
     assert measure("C2", 1) == want
+
+
+def test_readings_policy_bounds_pixels_over_max_err():
+    """Round 4: replay-diagnosed pixels may exceed MAX_ERR only about as often
+    as the readings' own (2x the worst reading's count + 3 sigma)."""
+    def rep(over):
+        r = _rep(700, 200, 0.07, max_err=0.5)
+        r["over_max_err"] = over
+        return r
+    ill = {"twin": _rep(400, 120, 0.08, max_err=0.3), "fma": _rep(380, 90, 0.05, max_err=0.2)}
+    ill["twin"]["over_max_err"], ill["fma"]["over_max_err"] = 3, 2
+    r = rep(12)
+    assert assert_parity_frame(r, ill) == "readings"          # 2 * 3 + 3 sqrt 6 = 13.3
+    assert r["readings_bound"]["over_max_err"] == pytest.approx(6 + 3 * 6 ** 0.5)
+    with pytest.raises(AssertionError):
+        assert_parity_frame(rep(14), ill)
+    # a full-size rate scales to the frame
+    full = {"strict_at_full_size": False, "width": 1000, "height": 1000,
+            "twin": {"outlier_rate": 4e-4, "undiagnosed_rate": 1.2e-4, "undiagnosed_max_err": 0.08,
+                     "over_max_err": 30},
+            "fma": {"outlier_rate": 4e-4, "undiagnosed_rate": 1.2e-4, "undiagnosed_max_err": 0.08,
+                    "over_max_err": 10}}
+    assert assert_parity_frame(rep(70), ill, full_size=full) == "readings"   # 60 + 3 sqrt 60
+
+
+def test_fast_regression_bounds():
+    """Full-size fast frames are held to the kernel's own last measurement
+    (tests/golden/fast_regression.json), inside the readings' spread."""
+    from parity import assert_regression, regression_bound
+    b = regression_bound("C5_p0")
+    m = b["measured"]
+    assert b["undiagnosed_max_err"] < 0.482      # tighter than the readings' magnitude
+    ok = {k: m[k] for k in ("outliers", "undiagnosed", "over_max_err", "undiagnosed_max_err",
+                            "max_err")}
+    assert assert_regression(dict(ok), "C5_p0") is not None
+    for k, v in (("undiagnosed", 2 * m["undiagnosed"]), ("undiagnosed_max_err", 0.45),
+                 ("over_max_err", 3 * m["over_max_err"] + 10)):
+        bad = dict(ok)
+        bad[k] = v
+        with pytest.raises(AssertionError):
+            assert_regression(bad, "C5_p0")
+    assert regression_bound("nope_p9") is None
+    for cfg in ("C2", "C3", "C4", "C5"):
+        assert regression_bound(f"{cfg}_p0") is not None
