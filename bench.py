@@ -95,8 +95,12 @@ def parse():
                          "slowest tiles finish); 1 serialises launches (profiling); "
                          "0 = 3 at N=1, 4 at N>1")
     ap.add_argument("--lag", type=int, default=2,
-                    help="N>1: frames between a frame's render and its gather (the host "
-                         "reads the frame's agreed stream lengths that much later)")
+                    help="N>1: frames between a batch's last render and its gather (the "
+                         "host reads the batch's agreed stream lengths that much later)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="N>1, native driver: frames per ship -- one RCCL length all-gather "
+                         "and one send/recv group per `batch` frames (0 = 2; needs "
+                         "streams %% batch == 0 and lag <= streams - batch)")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="frame loop: native = sdf_driver_* (C++, RCCL called directly); "
                          "python = multigpu.FrameDriver over torch.distributed")
@@ -347,7 +351,10 @@ def main():
     t_equal = R.tiling(rank, world, 8)
     rows = R.owned_rows(H, t)
     nbuf = args.streams or (3 if world == 1 else 4)
-    lag = min(args.lag, nbuf - 1) if nbuf > 1 else 1
+    batch = (args.batch or 2) if world > 1 else 1
+    if nbuf % batch:
+        batch = 1
+    lag = min(args.lag, nbuf - batch) if nbuf > batch else 1
 
     open_drivers = []   # closed before the process group goes
 
@@ -366,7 +373,7 @@ def main():
                 drv = NativeFrameDriver(f32, rank, world, dev, shares=shares, nbuf=nbuf,
                                         lag=lag if world > 1 else 1,
                                         dist=dist if world > 1 else None,
-                                        rccl_path=args.comm_lib)
+                                        rccl_path=args.comm_lib, batch=batch)
             except Exception as e:  # noqa: BLE001 - reported, then the fallback
                 log(f"[bench] rank {rank}: native driver unavailable ({e})")
                 ok = False
@@ -583,8 +590,9 @@ def main():
     driver_desc = ("native (sdf_driver_*, C++)" if native
                    else "python (multigpu.FrameDriver, torch.distributed)")
     if native:
-        gather_desc = ("RCCL all-gather of the TILES stream lengths + RCCL send/recv of "
-                       "exactly those bytes to rank 0 + sdf_tiles_decode_tilings")
+        gather_desc = (f"per batch of {batch} frames: one RCCL all-gather of the TILES stream "
+                       "lengths + one RCCL send/recv group of exactly those bytes to rank 0; "
+                       "sdf_tiles_decode_tilings per frame")
     else:
         gather_desc = (f"{'RCCL' if args.backend == 'nccl' else 'gloo'} gather to rank 0 + "
                        + ("sdf_tiles_decode_tilings" if wire == "tiles" else "sdf_deinterleave"))
@@ -605,7 +613,8 @@ def main():
                                   if world > 1 else "whole frame"),
                        "gather": gather_desc if world > 1 else None,
                        "driver": driver_desc,
-                       "streams": nbuf, "lag": lag if world > 1 else None},
+                       "streams": nbuf, "lag": lag if world > 1 else None,
+                       "batch": batch if (world > 1 and native) else None},
             "fps": round(args.steps / elapsed, 2),
             "frame_verified": verified,
             "display_rgba8": display,

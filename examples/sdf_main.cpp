@@ -89,15 +89,18 @@ int run_driver(sdf::Frame f, int frames, const std::string& out) {
   // shares: SDF3D_SHARES="a:b", else what the cost model of bench.py picks
   // for this world size (sdf3d_amd/multigpu.py choose_shares)
   static const int kShares[9][2] = {{1, 1}, {1, 1}, {1, 1}, {1, 1}, {3, 4},
-                                    {3, 4}, {1, 2}, {1, 2}, {1, 3}};
+                                    {3, 4}, {1, 2}, {1, 2}, {2, 7}};
   int share_root = kShares[world < 9 ? world : 8][0], share_peer = kShares[world < 9 ? world : 8][1];
   if (std::sscanf(env("SDF3D_SHARES", "").c_str(), "%d:%d", &share_root, &share_peer) != 2) {
     share_root = kShares[world < 9 ? world : 8][0];
     share_peer = kShares[world < 9 ? world : 8][1];
   }
-  sdf_driver_config cfg = {rank, world, share_root, share_peer, world > 1 || peer_root ? 4 : 3,
-                           world > 1 || peer_root ? 2 : 1,
-                           peer_root ? SDF_DRIVER_ROOT_AS_PEER : 0, 60000};
+  // N > 1: frames shipped two at a time (one length all-gather and one
+  // send/recv group per pair), 4 buffer sets, a pair gathered 2 frames after
+  // its last render
+  const bool ship = world > 1 || peer_root;
+  sdf_driver_config cfg = {rank, world, share_root, share_peer, ship ? 4 : 3, ship ? 2 : 1,
+                           peer_root ? SDF_DRIVER_ROOT_AS_PEER : 0, 60000, ship ? 2 : 1};
   f.params.output_format = SDF_FORMAT_RGBA32F;
   sdf::FrameDriver drv(f, cfg, lengths.get(), data.get());
   int64_t last = -1;

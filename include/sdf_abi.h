@@ -56,10 +56,12 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 9   /* 7: sdf_comm_create timeout, sdf_render_multi;
+#define SDF_ABI_VERSION 10  /* 7: sdf_comm_create timeout, sdf_render_multi;
                                 8: sdf_render_frames;
                                 9: TILES carries shading terms (64-byte
-                                   stream header), SDF_FORMAT_SHADE32F */
+                                   stream header), SDF_FORMAT_SHADE32F;
+                                10: sdf_driver_config.batch (frames per
+                                   ship) */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -466,10 +468,14 @@ int sdf_comm_destroy(sdf_comm* comm);
 typedef struct {
   int32_t rank, world;
   int32_t share_root, share_peer; /* blocks per period (>= 1; 1:1 = plain interleave) */
-  int32_t nbuf;                   /* buffer sets / render streams, 2 .. 16             */
-  int32_t lag;                    /* frames from render to gather, 1 .. nbuf - 1      */
+  int32_t nbuf;                   /* buffer sets, 2 .. 16 (render streams: <= 4)      */
+  int32_t lag;                    /* frames from a batch's last render to its gather,
+                                     1 .. nbuf - batch                                */
   int32_t flags;                  /* SDF_DRIVER_*                                     */
   int32_t timeout_ms;             /* host waits give up after this (<= 0: 60000)      */
+  int32_t batch;                  /* frames per ship (<= 0: 1): one length
+                                     all-gather and one send/recv group per `batch`
+                                     consecutive frames; nbuf % batch == 0          */
 } sdf_driver_config;
 
 /* The frame format is params->output_format (RGBA32F at world > 1: the wire

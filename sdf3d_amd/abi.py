@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 9
+SDF_ABI_VERSION = 10
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -99,13 +99,13 @@ class sdf_tiling(C.Structure):
 class sdf_driver_config(C.Structure):
     _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("share_root", C.c_int32),
                 ("share_peer", C.c_int32), ("nbuf", C.c_int32), ("lag", C.c_int32),
-                ("flags", C.c_int32), ("timeout_ms", C.c_int32)]
+                ("flags", C.c_int32), ("timeout_ms", C.c_int32), ("batch", C.c_int32)]
 
 
 STRUCT_SIZES = {
     "sdf_primitive": 64, "sdf_scene": 8 + 64 * SDF_MAX_PRIMS + 32, "sdf_camera": 88,
     "sdf_light": 32, "sdf_material": 40, "sdf_params": 80, "sdf_tiling": 24,
-    "sdf_driver_config": 32,
+    "sdf_driver_config": 36,
 }
 
 # every entry point of include/sdf_abi.h: name -> (restype, argtypes)

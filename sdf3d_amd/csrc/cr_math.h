@@ -27,9 +27,13 @@
 //
 // Every fast path is taken by a lane only where it is proven or checked
 // bit-identical; the fall-backs run in a branch the wave skips when no lane
-// needs it.  tests/crmath/crmath_check.hip runs these functions EXHAUSTIVELY
-// on the GPU (all 2^32 inputs for cr_sqrt and cr_log; the smooth-min domain
-// for div_prepared) against the generic sequences (tests/test_gpu_crmath.py).
+// needs it.  tests/crmath/crmath_check.hip runs cr_sqrt and cr_log
+// EXHAUSTIVELY on the GPU (all 2^32 inputs) and rcp_fast on every float of its
+// domain, against the generic sequences (tests/test_gpu_crmath.py).
+// div_scaled's domain, the (k, n) pairs of the smooth-min, has ~2^64 points:
+// it is SAMPLED (2^32 pairs, k log-uniform over every positive float, plus
+// denormal k, k near FLT_MAX and n whose scaled value underflows); its
+// bit-identity rests on Markstein's theorem, not on the sample.
 #pragma once
 
 #ifndef __HIPCC_RTC__

@@ -10,17 +10,24 @@
 // loop through torch.distributed costs ~0.12 ms of host time per frame,
 // tools/driver_probe.py).
 //
-// Per step i on rank r (b = i mod nbuf):
+// Frames are shipped in BATCHES of `batch` consecutive frames (round 4:
+// one length all-gather and one send/recv group per batch instead of per
+// frame, so rank 0's host calls and RCCL launches per frame shrink by the
+// batch).  Per step i on rank r (b = i mod nbuf):
 //   rs[b]  render(i): rank 0 its rows into frame[b] in place, the others
-//          their TILES stream into local[b]                     -> ev_render[b]
-//   ship(i - lag), if one is due (b' its buffer set):
-//     host   wait ev_size[b']: every rank's stream length of frame i - lag
-//     ds     wait ev_render[b']; group { send local[b'] (exactly its length)
-//            to rank 0 | rank 0: recv every peer's into gathered[b'] }
-//                                                                -> ev_gather[b']
-//     rs[b'] wait ev_gather[b']; rank 0: decode gathered[b'] into frame[b']
-//   ss     wait ev_render[b]; all-gather of the stream lengths of frame i;
-//          copy to pinned host memory                           -> ev_size[b]
+//          their TILES stream into local[b]; the compaction also writes the
+//          stream's length into lens[b]                         -> ev_render[b]
+//   ship every batch whose last frame is <= i - lag (g its slot):
+//     host   wait ev_size[g]: every rank's stream lengths of the batch
+//     ds     wait ev_render of its frames; group { send each local[b']
+//            (exactly its length) to rank 0 | rank 0: recv every peer's into
+//            gathered[b'] }                                      -> ev_gather[g]
+//     rs[b'] wait ev_gather[g]; rank 0: decode gathered[b'] into frame[b']
+//   if frame i ends a batch (slot g, first buffer b0):
+//     ss     wait ev_render of its frames; all-gather of lens[b0 .. b0 +
+//            batch) (batch int32 per rank); copy to pinned host -> ev_size[g]
+// nbuf % batch == 0, so a batch's lengths are contiguous; lag <= nbuf - batch,
+// so a batch is shipped before any of its buffer sets is rendered again.
 // Two communicators, each used from one stream only (as torch's process
 // groups are): the lengths on ss, the streams on ds.  Every rank issues the
 // same RCCL calls in the same order on each, and the two overlap: a frame's
@@ -61,6 +68,9 @@ struct Rccl {
   // thread runs the blocking ncclCommInitRank
   ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  // optional: flushes a communicator before it is destroyed; a non-blocking
+  // one answers ncclInProgress until that is done (sdf_comm_destroy)
+  ncclResult_t (*CommFinalize)(ncclComm_t) = nullptr;
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
@@ -101,6 +111,7 @@ Rccl* load_rccl(const char* path) {
   sym(r->GroupEnd, "ncclGroupEnd");
   r->CommInitRankConfig = reinterpret_cast<decltype(r->CommInitRankConfig)>(
       dlsym(h, "ncclCommInitRankConfig"));
+  r->CommFinalize = reinterpret_cast<decltype(r->CommFinalize)>(dlsym(h, "ncclCommFinalize"));
   if (!ok) {
     delete r;
     dlclose(h);
@@ -121,6 +132,7 @@ struct sdf_comm {
 struct sdf_driver {
   int dev = 0;
   int W = 0, H = 0, rank = 0, world = 1, nbuf = 0, lag = 1, flags = 0, timeout_ms = 60000;
+  int batch = 1, ngroups = 0;       // frames per ship; batch slots (nbuf / batch)
   bool collectives = false;  // anything shipped at all
   bool sender = false;       // this rank ships a TILES stream
   bool root = false;
@@ -138,15 +150,32 @@ struct sdf_driver {
   std::vector<char> sends;          // rank r ships a stream
   long long pitch = 0;              // gathered part pitch
   std::vector<void*> local, frames, gathered;
-  int32_t* sizes_dev = nullptr;
+  int32_t* sizes_dev = nullptr;     // per batch slot: batch int32 per rank (all-gathered)
   int32_t* sizes_host = nullptr;
   int32_t* zero_dev = nullptr;
+  uint32_t* lens_dev = nullptr;     // per buffer set: its stream's length (tiles_move)
   std::vector<sdf::RenderPlan> plan_send, plan_frame;
   sdf::DecodeParts decode{};
-  std::vector<hipStream_t> rs;
+  std::vector<hipStream_t> rs;      // per buffer set (at most kRenderStreams distinct)
+  std::vector<hipStream_t> streams;  // the distinct render streams
   hipStream_t ss = nullptr, ds = nullptr;
-  std::vector<hipEvent_t> ev_render, ev_size, ev_gather;
-  std::deque<long long> pending;
+  std::vector<hipEvent_t> ev_render;          // per buffer set
+  std::vector<hipEvent_t> ev_size, ev_gather;  // per batch slot
+  struct Batch {
+    long long first;   // frame index
+    int n;             // frames (< batch only for the one a drain closes)
+    int b0;            // buffer set of the first frame (the rest follow it)
+    int g;             // batch slot
+  };
+  std::deque<Batch> pending;
+  long long batch_first = 0;   // first frame of the batch being stepped
+  int buf_next = 0;            // buffer set of the next frame
+  long long nbatches = 0;      // batches closed so far (slot = nbatches mod ngroups)
+  // frame index -> buffer set of the last nbuf frames (ring at index mod nbuf):
+  // a drain that closes a short batch moves the next batch to the next
+  // multiple of `batch`, so that every batch's buffer sets (and lengths) are
+  // contiguous
+  std::vector<std::pair<long long, int>> frame_buf;
   long long next = 0;
   long long shipped = -1;  // highest frame whose streams are shipped and decoded (rank 0)
   int error = SDF_OK;  // sticky: a failed driver refuses further frames
@@ -239,46 +268,86 @@ int wait_event(sdf_driver* d, hipEvent_t e) {
   return host_wait(d, [e] { return hipEventQuery(e); });
 }
 
-// ship(j): the agreed lengths are on the host; move the streams to rank 0
-// and decode them there.
-int ship(sdf_driver* d, long long j) {
-  const int b = (int)(j % d->nbuf);
-  int rc = wait_event(d, d->ev_size[b]);
+// ship(batch): the agreed lengths are on the host; move the batch's streams
+// to rank 0 in one group and decode them there.
+int ship(sdf_driver* d, const sdf_driver::Batch& bt) {
+  const int g = bt.g;
+  int rc = wait_event(d, d->ev_size[g]);
   if (rc != SDF_OK) return rc;
-  const int32_t* sz = d->sizes_host + (size_t)b * d->world;
-  for (int r = 0; r < d->world; ++r)
-    if (d->sends[r] && (sz[r] < 0 || d->data_off[r] + sz[r] > d->stream_end[r]))
-      return fail(d, SDF_E_COMM);  // a length no stream of that rank can have
-  rc = hip_ok(hipStreamWaitEvent(d->ds, d->ev_render[b], 0));
+  // rank r's length of the batch's f-th frame: sz[r * batch + f]
+  const int32_t* sz = d->sizes_host + (size_t)g * d->batch * d->world;
+  for (int f = 0; f < bt.n; ++f)
+    for (int r = 0; r < d->world; ++r) {
+      const int32_t n = sz[(size_t)r * d->batch + f];
+      if (d->sends[r] && (n < 0 || d->data_off[r] + n > d->stream_end[r]))
+        return fail(d, SDF_E_COMM);  // a length no stream of that rank can have
+    }
+  for (int f = 0; f < bt.n && rc == SDF_OK; ++f)
+    rc = hip_ok(hipStreamWaitEvent(d->ds, d->ev_render[bt.b0 + f], 0));
   if (rc != SDF_OK) return fail(d, rc);
   const Rccl& R = *d->data_comm->api;
   ncclComm_t comm = d->data_comm->comm;
   auto tg = Clock::now();
   rc = nccl_ok(R.GroupStart());
-  if (rc == SDF_OK && d->sender)
-    rc = nccl_ok(R.Send(d->local[b], (size_t)(d->data_off[d->rank] + sz[d->rank]), ncclUint8, 0,
-                        comm, d->ds));
-  if (d->root)
-    for (int r = 0; r < d->world && rc == SDF_OK; ++r)
-      if (d->sends[r])
-        rc = nccl_ok(R.Recv(static_cast<char*>(d->gathered[b]) + (size_t)r * d->pitch,
-                            (size_t)(d->data_off[r] + sz[r]), ncclUint8, r, comm, d->ds));
+  for (int f = 0; f < bt.n && rc == SDF_OK; ++f) {
+    const int b = bt.b0 + f;
+    if (d->sender)
+      rc = nccl_ok(R.Send(d->local[b],
+                          (size_t)(d->data_off[d->rank] + sz[(size_t)d->rank * d->batch + f]),
+                          ncclUint8, 0, comm, d->ds));
+    if (d->root)
+      for (int r = 0; r < d->world && rc == SDF_OK; ++r)
+        if (d->sends[r])
+          rc = nccl_ok(R.Recv(static_cast<char*>(d->gathered[b]) + (size_t)r * d->pitch,
+                              (size_t)(d->data_off[r] + sz[(size_t)r * d->batch + f]), ncclUint8,
+                              r, comm, d->ds));
+  }
   // (a non-blocking communicator may still be enqueueing: settle before the
   // event below is recorded behind the group's kernels)
   const int rc_end = nccl_ok(settle(d->data_comm, R.GroupEnd(), d->timeout_ms));
   d->t_group += seconds_since(tg);
   if (rc == SDF_OK) rc = rc_end;
   if (rc != SDF_OK) return fail(d, rc);
-  rc = hip_ok(hipEventRecord(d->ev_gather[b], d->ds));
-  if (rc == SDF_OK) rc = hip_ok(hipStreamWaitEvent(d->rs[b], d->ev_gather[b], 0));
-  if (rc == SDF_OK && d->root) {
-    tg = Clock::now();
-    rc = hip_ok((hipError_t)sdf::launch_tiles_decode(d->decode, d->frames[b], d->gathered[b],
-                                                     d->rs[b]));
-    d->t_decode += seconds_since(tg);
+  rc = hip_ok(hipEventRecord(d->ev_gather[g], d->ds));
+  for (int f = 0; f < bt.n && rc == SDF_OK; ++f) {
+    const int b = bt.b0 + f;
+    rc = hip_ok(hipStreamWaitEvent(d->rs[b], d->ev_gather[g], 0));
+    if (rc == SDF_OK && d->root) {
+      tg = Clock::now();
+      rc = hip_ok((hipError_t)sdf::launch_tiles_decode(d->decode, d->frames[b], d->gathered[b],
+                                                       d->rs[b]));
+      d->t_decode += seconds_since(tg);
+    }
   }
-  if (rc == SDF_OK) d->shipped = j;
+  if (rc == SDF_OK) d->shipped = bt.first + bt.n - 1;
   return fail(d, rc);
+}
+
+// The stream lengths of the batch [first, first + n) to every rank: one
+// all-gather of `batch` int32 per rank (entries past n are ignored), copied
+// to pinned host memory; the batch then waits in `pending` for its ship.
+int gather_lengths(sdf_driver* d, long long first, int n, int b0) {
+  const auto tr = Clock::now();
+  const int g = (int)(d->nbatches++ % d->ngroups);
+  int rc = SDF_OK;
+  for (int f = 0; f < n && rc == SDF_OK; ++f)
+    rc = hip_ok(hipStreamWaitEvent(d->ss, d->ev_render[b0 + f], 0));
+  if (rc != SDF_OK) return fail(d, rc);
+  int32_t* sz = d->sizes_dev + (size_t)g * d->batch * d->world;
+  const void* src = d->sender ? (const void*)(d->lens_dev + b0) : (const void*)d->zero_dev;
+  rc = nccl_ok(settle(d->size_comm,
+                      d->size_comm->api->AllGather(src, sz, (size_t)d->batch, ncclInt32,
+                                                   d->size_comm->comm, d->ss),
+                      d->timeout_ms));
+  if (rc == SDF_OK)
+    rc = hip_ok(hipMemcpyAsync(d->sizes_host + (size_t)g * d->batch * d->world, sz,
+                               sizeof(int32_t) * d->batch * d->world, hipMemcpyDeviceToHost,
+                               d->ss));
+  if (rc == SDF_OK) rc = hip_ok(hipEventRecord(d->ev_size[g], d->ss));
+  d->t_lengths += seconds_since(tr);
+  if (rc != SDF_OK) return fail(d, rc);
+  d->pending.push_back({first, n, b0, g});
+  return SDF_OK;
 }
 
 void release(sdf_driver* d) {
@@ -288,8 +357,9 @@ void release(sdf_driver* d) {
       if (p) (void)hipFree(p);
   if (d->sizes_dev) (void)hipFree(d->sizes_dev);
   if (d->zero_dev) (void)hipFree(d->zero_dev);
+  if (d->lens_dev) (void)hipFree(d->lens_dev);
   if (d->sizes_host) (void)hipHostFree(d->sizes_host);
-  for (hipStream_t s : d->rs)
+  for (hipStream_t s : d->streams)
     if (s) (void)hipStreamDestroy(s);
   if (d->ss) (void)hipStreamDestroy(d->ss);
   if (d->ds) (void)hipStreamDestroy(d->ds);
@@ -384,10 +454,31 @@ int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32
   return SDF_OK;
 }
 
+// A communicator created non-blocking may answer ncclInProgress while RCCL
+// tears it down.  Where RCCL has ncclCommFinalize, the
+// communicator is finalised first and polled to completion (settle; rccl.h:
+// the state becomes ncclSuccess once it is globally quiescent), then
+// destroyed, which then only frees local resources; a finalise that fails or
+// times out aborts the communicator instead.  Without ncclCommFinalize the
+// destroy is the whole teardown (an ncclInProgress answer is not an error:
+// the handle is gone, so there is nothing left to poll).
 int sdf_comm_destroy(sdf_comm* comm) {
   if (!comm) return SDF_OK;
   int rc = SDF_OK;
-  if (comm->comm) rc = nccl_ok(comm->api->CommDestroy(comm->comm));
+  if (comm->comm) {
+    const int limit = 60000;
+    if (comm->api->CommFinalize) {
+      rc = nccl_ok(settle(comm, comm->api->CommFinalize(comm->comm), limit));
+      if (rc != SDF_OK) {
+        comm->api->CommAbort(comm->comm);
+        comm->comm = nullptr;
+      }
+    }
+    if (comm->comm) {
+      const ncclResult_t d = comm->api->CommDestroy(comm->comm);
+      if (rc == SDF_OK) rc = nccl_ok(d == ncclInProgress ? ncclSuccess : d);
+    }
+  }
   delete comm;
   return rc;
 }
@@ -399,9 +490,11 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
   if (!config || !driver || !params) return SDF_E_INVALID_ARG;
   *driver = nullptr;
   const sdf_driver_config& c = *config;
+  const int batch = c.batch > 0 ? c.batch : 1;
   if (c.world < 1 || c.world > SDF_MAX_DECODE_PARTS || c.rank < 0 || c.rank >= c.world ||
       c.share_root < 1 || c.share_peer < 1 || c.nbuf < 2 || c.nbuf > 16 || c.lag < 1 ||
-      c.lag > c.nbuf - 1 || (c.flags & ~SDF_DRIVER_ROOT_AS_PEER) != 0)
+      batch > 16 || c.nbuf % batch != 0 || c.lag > c.nbuf - batch ||
+      (c.flags & ~SDF_DRIVER_ROOT_AS_PEER) != 0)
     return SDF_E_INVALID_ARG;
   const bool peer_root = (c.flags & SDF_DRIVER_ROOT_AS_PEER) != 0;
   const bool collectives = c.world > 1 || peer_root;
@@ -427,6 +520,9 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
   d->world = c.world;
   d->nbuf = c.nbuf;
   d->lag = c.lag;
+  d->batch = batch;
+  d->ngroups = c.nbuf / batch;
+  d->frame_buf.assign(c.nbuf, {-1, 0});
   d->flags = c.flags;
   d->timeout_ms = c.timeout_ms > 0 ? c.timeout_ms : 60000;
   d->collectives = collectives;
@@ -469,15 +565,21 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
   auto alloc = [&](void** p, size_t n) {
     return rc == SDF_OK ? (rc = hip_ok(hipMalloc(p, n ? n : 16))) : rc;
   };
+  // render streams: one per buffer set, at most kRenderStreams distinct
+  // (buffer set b on stream b mod kRenderStreams): with the two
+  // communication streams they fit HIP's hardware queues (bench.py: 8)
+  constexpr int kRenderStreams = 4;
+  d->streams.assign(std::min(c.nbuf, kRenderStreams), nullptr);
+  for (hipStream_t& st : d->streams)
+    if (rc == SDF_OK) rc = hip_ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   d->rs.assign(c.nbuf, nullptr);
+  for (int b = 0; b < c.nbuf; ++b) d->rs[b] = d->streams[b % d->streams.size()];
   d->ev_render.assign(c.nbuf, nullptr);
-  d->ev_size.assign(c.nbuf, nullptr);
-  d->ev_gather.assign(c.nbuf, nullptr);
-  for (int b = 0; b < c.nbuf && rc == SDF_OK; ++b) {
-    rc = hip_ok(hipStreamCreateWithFlags(&d->rs[b], hipStreamNonBlocking));
-    for (auto* v : {&d->ev_render, &d->ev_size, &d->ev_gather})
-      if (rc == SDF_OK) rc = hip_ok(hipEventCreateWithFlags(&(*v)[b], hipEventDisableTiming));
-  }
+  d->ev_size.assign(d->ngroups, nullptr);
+  d->ev_gather.assign(d->ngroups, nullptr);
+  for (auto* v : {&d->ev_render, &d->ev_size, &d->ev_gather})
+    for (hipEvent_t& e : *v)
+      if (rc == SDF_OK) rc = hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (rc == SDF_OK) rc = hip_ok(hipStreamCreateWithFlags(&d->ss, hipStreamNonBlocking));
   if (rc == SDF_OK) rc = hip_ok(hipStreamCreateWithFlags(&d->ds, hipStreamNonBlocking));
   d->local.assign(c.nbuf, nullptr);
@@ -485,6 +587,11 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
   d->gathered.assign(c.nbuf, nullptr);
   d->plan_send.resize(c.nbuf);
   d->plan_frame.resize(c.nbuf);
+  if (d->sender) {
+    // every buffer set's stream length (a rank that owns no rows keeps 0)
+    alloc((void**)&d->lens_dev, sizeof(uint32_t) * c.nbuf);
+    if (rc == SDF_OK) rc = hip_ok(hipMemset(d->lens_dev, 0, sizeof(uint32_t) * c.nbuf));
+  }
   for (int b = 0; b < c.nbuf && rc == SDF_OK; ++b) {
     if (d->sender) {
       alloc(&d->local[b], local_bytes);
@@ -493,6 +600,7 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
       if (rc == SDF_OK)
         rc = sdf::make_render_plan(scene, camera, light, material, &pt, &d->tilings[c.rank],
                                    d->local[b], nullptr, &d->plan_send[b]);
+      d->plan_send[b].tiles_used = d->lens_dev + b;
     }
     if (d->root) {
       alloc(&d->frames[b], frame_bytes);
@@ -513,8 +621,9 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
     }
   }
   if (collectives && rc == SDF_OK) {
+    // batch slots x batch frames x world ranks (= nbuf x world)
     alloc((void**)&d->sizes_dev, sizeof(int32_t) * c.nbuf * c.world);
-    alloc((void**)&d->zero_dev, 64);
+    alloc((void**)&d->zero_dev, 64);   // a non-sending rank's lengths (batch <= 16)
     if (rc == SDF_OK) rc = hip_ok(hipMemset(d->zero_dev, 0, 64));
     if (rc == SDF_OK)
       rc = hip_ok(hipHostMalloc((void**)&d->sizes_host, sizeof(int32_t) * c.nbuf * c.world,
@@ -568,7 +677,7 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
   if (d->error != SDF_OK) return d->error;
   if (hipSetDevice(d->dev) != hipSuccess) return fail(d, SDF_E_HIP);
   const long long i = d->next;
-  const int b = (int)(i % d->nbuf);
+  const int b = d->buf_next;
   hipStream_t s = d->rs[b];
   int rc = SDF_OK;
   auto tr = Clock::now();
@@ -578,32 +687,26 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
   if (rc != SDF_OK) return fail(d, rc);
   if (frame_index) *frame_index = i;
   d->next = i + 1;
+  d->frame_buf[i % d->nbuf] = {i, b};
+  d->buf_next = (b + 1) % d->nbuf;
   if (!d->collectives) return SDF_OK;
   rc = hip_ok(hipEventRecord(d->ev_render[b], s));
   if (rc != SDF_OK) return fail(d, rc);
-  // frame i - lag: its lengths are on the host by now (lag >= 2: long since)
-  if ((int)d->pending.size() >= d->lag) {
-    const long long j = d->pending.front();
+  // batches whose last frame is at least `lag` frames old: their lengths are
+  // on the host by now (lag >= 2: long since)
+  while (!d->pending.empty() &&
+         d->pending.front().first + d->pending.front().n - 1 <= i - d->lag) {
+    const sdf_driver::Batch bt = d->pending.front();
     d->pending.pop_front();
-    rc = ship(d, j);
+    rc = ship(d, bt);
     if (rc != SDF_OK) return rc;
   }
-  // the ranks' stream lengths of frame i, to every rank
-  tr = Clock::now();
-  rc = hip_ok(hipStreamWaitEvent(d->ss, d->ev_render[b], 0));
-  if (rc != SDF_OK) return fail(d, rc);
-  int32_t* sz = d->sizes_dev + (size_t)b * d->world;
-  rc = nccl_ok(settle(d->size_comm,
-                      d->size_comm->api->AllGather(d->sender ? d->local[b] : (void*)d->zero_dev,
-                                                   sz, 1, ncclInt32, d->size_comm->comm, d->ss),
-                      d->timeout_ms));
-  if (rc == SDF_OK)
-    rc = hip_ok(hipMemcpyAsync(d->sizes_host + (size_t)b * d->world, sz,
-                               sizeof(int32_t) * d->world, hipMemcpyDeviceToHost, d->ss));
-  if (rc == SDF_OK) rc = hip_ok(hipEventRecord(d->ev_size[b], d->ss));
-  d->t_lengths += seconds_since(tr);
-  if (rc != SDF_OK) return fail(d, rc);
-  d->pending.push_back(i);
+  // frame i ends a batch: its lengths to every rank
+  if (i + 1 - d->batch_first == d->batch) {
+    const long long first = d->batch_first;
+    d->batch_first = i + 1;
+    return gather_lengths(d, first, d->batch, b + 1 - d->batch);
+  }
   return SDF_OK;
 }
 
@@ -620,13 +723,25 @@ int sdf_driver_drain(sdf_driver* d) {
 static int driver_drain(sdf_driver* d) {
   if (d->error != SDF_OK) return d->error;
   if (hipSetDevice(d->dev) != hipSuccess) return fail(d, SDF_E_HIP);
-  while (!d->pending.empty()) {
-    const long long j = d->pending.front();
-    d->pending.pop_front();
-    const int rc = ship(d, j);
+  // a batch the last steps began but did not complete goes as it is (every
+  // rank has stepped the same frames)
+  if (d->collectives && d->next > d->batch_first) {
+    const long long first = d->batch_first;
+    const int n = (int)(d->next - first);
+    const int b0 = (d->buf_next - n + d->nbuf) % d->nbuf;
+    d->batch_first = d->next;
+    // the next batch starts on a multiple of `batch` (contiguous buffer sets)
+    d->buf_next = (d->buf_next + d->batch - 1) / d->batch * d->batch % d->nbuf;
+    const int rc = gather_lengths(d, first, n, b0);
     if (rc != SDF_OK) return rc;
   }
-  std::vector<hipStream_t> all = d->rs;
+  while (!d->pending.empty()) {
+    const sdf_driver::Batch bt = d->pending.front();
+    d->pending.pop_front();
+    const int rc = ship(d, bt);
+    if (rc != SDF_OK) return rc;
+  }
+  std::vector<hipStream_t> all = d->streams;
   all.push_back(d->ss);
   all.push_back(d->ds);
   for (hipStream_t s : all) {
@@ -644,7 +759,9 @@ int sdf_driver_frame(sdf_driver* d, int64_t index, void** rgba) {
   // with collectives a frame holds the peers' rows only once it has been
   // shipped (the last `lag` frames stepped: after sdf_driver_drain)
   if (d->collectives && index > d->shipped) return SDF_E_INVALID_ARG;
-  *rgba = d->frames[index % d->nbuf];
+  const auto& fb = d->frame_buf[index % d->nbuf];
+  if (fb.first != index) return SDF_E_INVALID_ARG;
+  *rgba = d->frames[fb.second];
   return SDF_OK;
 }
 
@@ -656,7 +773,7 @@ int sdf_driver_read_frame(sdf_driver* d, int64_t index, void* dst, int64_t bytes
   if (!dst || bytes < (int64_t)n) return SDF_E_INVALID_ARG;
   if (hipSetDevice(d->dev) != hipSuccess) return SDF_E_HIP;
   // after everything queued for the frame's buffer set (render, decode)
-  const int b = (int)(index % d->nbuf);
+  const int b = d->frame_buf[index % d->nbuf].second;
   hipEvent_t e = nullptr;
   rc = hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (rc == SDF_OK) rc = hip_ok(hipEventRecord(e, d->rs[b]));

@@ -59,8 +59,16 @@ DeviceFrames* device_state(int dev) {
     auto* d = new DeviceFrames;
     d->counters = static_cast<uint8_t*>(p);
     d->blocks = cus * 8;   // 256-thread groups: 4 waves each, 32 waves per CU
-    for (hipEvent_t& e : d->done)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    for (hipEvent_t& e : d->done) {
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) continue;
+      // undo this attempt whole: the next call starts afresh
+      e = nullptr;
+      for (hipEvent_t& x : d->done)
+        if (x) (void)hipEventDestroy(x);
+      (void)hipFree(d->counters);
+      delete d;
+      return nullptr;
+    }
     g_dev[dev] = d;
   }
   return g_dev[dev];

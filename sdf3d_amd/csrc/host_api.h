@@ -22,6 +22,7 @@ struct RenderPlan {
   int nsig;
   int rows;                // 0: nothing to render
   int tiles_ntiles;        // > 0: TILES output, compacted after the render
+  uint32_t* tiles_used = nullptr;   // TILES: also receives the stream's length (device)
 };
 
 // Rows a tiling owns (sdf_owned_rows), or SDF_E_INVALID_ARG.

@@ -156,7 +156,10 @@ struct TilesLayout {
     end = slots + n * kTilePlaneBytes;
   }
 };
-int launch_tiles_compact(void* stream_buf, int ntiles, void* stream);
+// `used_out` (may be null): a device word that also receives the stream's
+// length (header word 0), e.g. one slot of the frame driver's lengths array
+// whose slots of consecutive frames are all-gathered in one call.
+int launch_tiles_compact(void* stream_buf, int ntiles, void* stream, uint32_t* used_out = nullptr);
 // A tile's head word 0 (sdf_abi.h SDF_FORMAT_TILES): base widths b0 | b1 << 6
 // | b2 << 12, the tile's data in qwords << 18, escaped channels << 26.
 __host__ __device__ inline uint32_t tile_qwords(uint32_t head) { return (head >> 18) & 255u; }

@@ -27,7 +27,7 @@ static_assert(sizeof(sdf_light) == 32, "sdf_light layout");
 static_assert(sizeof(sdf_material) == 40, "sdf_material layout");
 static_assert(sizeof(sdf_params) == 80, "sdf_params layout");
 static_assert(sizeof(sdf_tiling) == 24, "sdf_tiling layout");
-static_assert(sizeof(sdf_driver_config) == 32, "sdf_driver_config layout");
+static_assert(sizeof(sdf_driver_config) == 36, "sdf_driver_config layout");
 
 namespace sdf {
 
@@ -456,7 +456,7 @@ int launch_render_plan(const RenderPlan& plan, void* stream) {
     err = plan.exact ? launch_render_exact(plan.a, plan.variant, stream)
                      : launch_render_fast(plan.a, plan.variant, stream);
   if (err == hipSuccess && plan.tiles_ntiles > 0)
-    err = launch_tiles_compact(plan.a.rgba, plan.tiles_ntiles, stream);
+    err = launch_tiles_compact(plan.a.rgba, plan.tiles_ntiles, stream, plan.tiles_used);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 

@@ -37,9 +37,14 @@ enum TilesShade : uint32_t {
 // Exact precision: pow in fp64, rounded to fp32 once (the oracle's cr_powf).
 // For an integer exponent n in [0, 64] (the shininess, a uniform; 12 by
 // default) x^n by repeated squaring in fp64 instead of the library pow (~130
-// fp64 instructions): x^2 is exact (48-bit product) and each further product
-// adds at most 2^-53 relative, so the value lies within n 2^-53 < 2^-46 of
-// x^n.  Where both ends of a 2^-44 interval around it round to the same
+// fp64 instructions).  Binary powering is one parenthesisation of the product
+// of n factors x: expanded as a product tree (a squared node's rounding error
+// counts once per use) it has n - 1 multiplications, so with u = 2^-53 the
+// value v satisfies |v / x^n - 1| <= (n - 1) u / (1 - (n - 1) u) < 2^-46 for
+// n <= 64 (no intermediate underflows where x^n is near a float: x <= 1 keeps
+// every partial product >= x^n, x > 1 keeps it >= 1).  The exhaustive GPU
+// comparison with the library pow for every n in [0, 64]
+// (tests/test_gpu_parity.py) checks it.  Where both ends of a 2^-44 interval around it round to the same
 // float, that float is the correct rounding of x^n -- and of the library's
 // fp64 pow, which lies in the same interval; other lanes (rounding
 // boundaries, NaN) take the library pow.  SDF_SHADE_LIBRARY_POW (the TILES

@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void tiles_scan(uint8_t* buf, int ntiles) {
 
 constexpr int kMoveTiles = 8;   // tiles per wave of tiles_move (divides kScanTiles)
 
-__global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles) {
+__global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles, uint32_t* used_out) {
   const TilesLayout L(ntiles);
   const int t0 = (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * kMoveTiles;
   if (t0 >= ntiles) return;
@@ -347,6 +347,7 @@ __global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles) {
       if (t0 + k == ntiles - 1) {
         reinterpret_cast<uint32_t*>(buf)[0] = off + (uint32_t)nq * 8u;
         reinterpret_cast<uint32_t*>(buf)[1] = (uint32_t)ntiles;
+        if (used_out) *used_out = off + (uint32_t)nq * 8u;
       }
     }
   }
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles) {
 
 }  // namespace
 
-int launch_tiles_compact(void* stream_buf, int ntiles, void* stream) {
+int launch_tiles_compact(void* stream_buf, int ntiles, void* stream, uint32_t* used_out) {
   if (ntiles <= 0) return 0;
   (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   uint8_t* buf = reinterpret_cast<uint8_t*>(stream_buf);
@@ -362,7 +363,7 @@ int launch_tiles_compact(void* stream_buf, int ntiles, void* stream) {
                      (hipStream_t)stream, buf, ntiles);
   const int waves = (ntiles + kMoveTiles - 1) / kMoveTiles;
   hipLaunchKernelGGL(tiles_move, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, buf,
-                     ntiles);
+                     ntiles, used_out);
   return (int)hipGetLastError();
 }
 

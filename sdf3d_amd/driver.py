@@ -100,11 +100,13 @@ class Comm:
 class NativeFrameDriver:
     """The frame loop in C++ (sdf_driver_*).  ``step()`` enqueues one frame;
     ``drain()`` ships everything and waits; ``read_frame(i, out)`` copies
-    rank 0's frame i (one of the last ``nbuf``) into a torch tensor."""
+    rank 0's frame i (one of the last ``nbuf``) into a torch tensor.
+    ``batch``: frames per ship (one length all-gather and one send/recv group
+    per batch; nbuf % batch == 0, lag <= nbuf - batch)."""
 
     def __init__(self, frame: Frame, rank: int, world: int, device, shares=(1, 1), nbuf: int = 4,
                  lag: int = 2, dist=None, root_as_peer: bool = False, timeout_ms: int = 60000,
-                 rccl_path: str | None = None):
+                 rccl_path: str | None = None, batch: int = 1):
         import torch
         self.torch = torch
         self.lib = abi.load_library()
@@ -115,7 +117,7 @@ class NativeFrameDriver:
         cfg = abi.sdf_driver_config(rank=rank, world=world, share_root=shares[0],
                                     share_peer=shares[1], nbuf=nbuf, lag=lag,
                                     flags=abi.DRIVER_ROOT_AS_PEER if root_as_peer else 0,
-                                    timeout_ms=timeout_ms)
+                                    timeout_ms=timeout_ms, batch=batch)
         if world > 1 or root_as_peer:
             if dist is None:
                 raise ValueError("a multi-rank driver needs torch.distributed for its comm ids")

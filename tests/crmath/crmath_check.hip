@@ -8,6 +8,14 @@
 //          (every positive finite k, n in [0, k]): bits, and h*h*k*0.25
 //          (what the smooth-min uses) -- 2^32 (k, n) pairs, k uniform in
 //          bits, n spread over [0, k] including tiny and denormal n
+//   sminedge : the same comparison on 2^32 pairs from four edge families
+//          (ADVICE r03): denormal k; k within 2^20 ulps of FLT_MAX; k >= 2^64
+//          with n so small that n * sc underflows; tiny normal k (2^-126 ..
+//          2^-100)
+//   pow  : shade.h spec_pow<exact>(x, n) (repeated squaring in fp64, the
+//          library pow on lanes near a rounding boundary) vs the library
+//          (float)pow((double)x, (double)n), for EVERY float x in [0, 1.0001]
+//          (spec_x = max(N.H, 0)) and every integer shininess n in [0, 64]
 // Prints one JSON line.  Built by sdf3d_amd/build.py (build_crmath_check);
 // run by tests/test_gpu_crmath.py.
 #include <hip/hip_runtime.h>
@@ -15,6 +23,7 @@
 #include <cstring>
 
 #include "../../sdf3d_amd/csrc/cr_math.h"
+#include "../../sdf3d_amd/csrc/shade.h"
 
 struct Counts {
   unsigned long long mismatch, fast, effective;
@@ -103,11 +112,67 @@ __global__ void check_smin(unsigned base, Counts* c) {
   tally(c, bad, true, eff, i);
 }
 
+// the smooth-min's host preparation and comparison (check_smin)
+__device__ __forceinline__ void smin_case(float k, float n, unsigned tag, Counts* c) {
+  const int e = __builtin_amdgcn_frexp_expf(k);
+  const float sc = __builtin_ldexpf(1.0f, (1 - e) < 127 ? (1 - e) : 127);
+  const float ys = 1.0f / (k * sc);
+  if (!(n <= k)) n = k;
+  const float a = sdf::crm::div_scaled(n, k, sc, ys), b = n / k;
+  const bool bad = !same_bits(a, b);
+  const bool eff = !same_bits(a * a * k * 0.25f, b * b * k * 0.25f);
+  tally(c, bad, true, eff, tag);
+}
+
+__global__ void check_smin_edges(unsigned base, Counts* c) {
+  const unsigned i = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned fam = i >> 30, ki = (i >> 12) & 0x3FFFFu, ni = i & 4095u;
+  const unsigned hk = hash32(ki * 0x9E3779B9u + fam), h = hash32(i * 2654435761u + 777u);
+  unsigned kbits;
+  switch (fam) {
+    case 0: kbits = 1u + hk % 0x007FFFFEu; break;                    // denormal k
+    case 1: kbits = 0x7F7FFFFFu - (hk & 0xFFFFFu); break;            // near FLT_MAX
+    case 2: kbits = 0x5F800000u + hk % (0x7F7FFFFFu - 0x5F800000u); break;   // k >= 2^64
+    default: kbits = 0x00800000u + hk % (0x0D800000u - 0x00800000u); break;  // 2^-126..2^-100
+  }
+  const float k = __uint_as_float(kbits);
+  float n;
+  if (fam == 2) {
+    // n * sc underflows: sc <= 2^-63, so any n below 2^-63 (denormal or tiny)
+    n = ni < 2048 ? __uint_as_float(h & 0x007FFFFFu)                  // denormal
+                  : __uint_as_float(0x00800000u + h % (0x20000000u - 0x00800000u));
+  } else if (ni < 2048) {
+    n = k * (__uint_as_float(0x3F800000u | (h >> 9)) - 1.0f);           // [0, k)
+  } else if (ni < 3584) {
+    n = __uint_as_float(h % kbits);                                     // any float below k
+  } else {
+    n = __uint_as_float(kbits - (h & 0xFFFu) < kbits ? kbits - (h & 0xFFFu) : 0u);   // near k
+  }
+  smin_case(k, n, i, c);
+}
+
+// x = index (bits) in [0, 0x3F800347) i.e. [0, 1.0001]; every n in [0, 64]
+constexpr unsigned kPowXEnd = 0x3F800347u;
+__global__ void check_pow(unsigned base, Counts* c) {
+  const unsigned u = base + blockIdx.x * blockDim.x + threadIdx.x;
+  // past the end: only the high lanes of the last wave (tally counts from
+  // lane 0, which is inside) and whole waves after it
+  if (u >= kPowXEnd) return;
+  const float x = __uint_as_float(u);
+  unsigned long long bad_n = 0ull;
+  for (int n = 0; n <= 64; n++) {
+    const float a = sdf::spec_pow<true>(x, (float)n);
+    const float b = (float)pow((double)x, (double)n);
+    if (!same_bits(a, b)) bad_n |= 1ull << (n & 63);
+  }
+  tally(c, bad_n != 0ull, true, bad_n != 0ull, u);
+}
+
 static int run(const char* name, void (*kern)(unsigned, Counts*), Counts* d, char* out,
-               size_t cap) {
+               size_t cap, unsigned long long end = 1ull << 32) {
   (void)hipMemset(d, 0, sizeof(Counts));
   const unsigned threads = 256, chunk = 1u << 28;
-  for (unsigned long long base = 0; base < (1ull << 32); base += chunk) {
+  for (unsigned long long base = 0; base < end; base += chunk) {
     hipLaunchKernelGGL(kern, dim3(chunk / threads), dim3(threads), 0, 0, (unsigned)base, d);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
   }
@@ -120,24 +185,43 @@ static int run(const char* name, void (*kern)(unsigned, Counts*), Counts* d, cha
     strncat(firsts, tmp, sizeof firsts - strlen(firsts) - 1);
   }
   return snprintf(out, cap, "\"%s\": {\"inputs\": %llu, \"mismatch\": %llu, \"effective\": %llu, "
-                  "\"fast_path\": %llu, \"first\": [%s]}", name, 1ull << 32, h.mismatch,
+                  "\"fast_path\": %llu, \"first\": [%s]}", name, end, h.mismatch,
                   h.effective, h.fast, firsts);
 }
 
 int main(int argc, char** argv) {
   Counts* d;
   if (hipMalloc(&d, sizeof(Counts)) != hipSuccess) return 2;
-  char a[400], b[400], c[400], r[400];
   const bool all = argc < 2;
-  const bool want_sqrt = all || strstr(argv[1], "sqrt"), want_log = all || strstr(argv[1], "log"),
-             want_smin = all || strstr(argv[1], "smin"), want_rcp = all || strstr(argv[1], "rcp");
-  a[0] = b[0] = c[0] = r[0] = 0;
-  if (want_rcp && run("rcp", check_rcp, d, r, sizeof r) < 0) return 3;
-  if (want_sqrt && run("sqrt", check_sqrt, d, a, sizeof a) < 0) return 3;
-  if (want_log && run("log", check_log, d, b, sizeof b) < 0) return 3;
-  if (want_smin && run("smin", check_smin, d, c, sizeof c) < 0) return 3;
-  printf("{%s%s%s%s%s%s%s}\n", r, (r[0] && (a[0] || b[0] || c[0])) ? ", " : "", a,
-         (a[0] && (b[0] || c[0])) ? ", " : "", b, (b[0] && c[0]) ? ", " : "", c);
+  struct Check {
+    const char* name;
+    void (*kern)(unsigned, Counts*);
+    unsigned long long end;
+    char out[400];
+  } checks[] = {{"rcp", check_rcp, 1ull << 32, ""},   {"sqrt", check_sqrt, 1ull << 32, ""},
+                {"log", check_log, 1ull << 32, ""},   {"smin", check_smin, 1ull << 32, ""},
+                {"sminedge", check_smin_edges, 1ull << 32, ""},
+                {"pow", check_pow, kPowXEnd, ""}};
+  // an argument selects checks by name (e.g. "sqrt,log"; "smin" matches only
+  // itself)
+  auto wanted = [&](const char* name) {
+    if (all) return true;
+    for (const char* p = argv[1]; (p = strstr(p, name)) != nullptr; p += strlen(name)) {
+      const char after = p[strlen(name)];
+      const bool start = p == argv[1] || p[-1] == ',';
+      if (start && (after == 0 || after == ',')) return true;
+    }
+    return false;
+  };
+  bool first = true;
+  printf("{");
+  for (Check& k : checks) {
+    if (!wanted(k.name)) continue;
+    if (run(k.name, k.kern, d, k.out, sizeof k.out, k.end) < 0) return 3;
+    printf("%s%s", first ? "" : ", ", k.out);
+    first = false;
+  }
+  printf("}\n");
   (void)hipFree(d);
   return 0;
 }

@@ -13,6 +13,8 @@ from __future__ import annotations
 import random
 import socket
 import subprocess
+import sys
+import warnings
 
 _ADDR_IN_USE = ("EADDRINUSE", "address already in use", "Address already in use")
 
@@ -36,8 +38,18 @@ def run_launcher(make_cmd, attempts: int = 2, **kw) -> subprocess.CompletedProce
     """subprocess.run(make_cmd(port), capture_output=True, text=True, **kw),
     launched again with a new port when the rendezvous could not listen."""
     r = None
-    for _ in range(attempts):
-        r = subprocess.run(make_cmd(free_port()), capture_output=True, text=True, **kw)
+    for attempt in range(attempts):
+        port = free_port()
+        r = subprocess.run(make_cmd(port), capture_output=True, text=True, **kw)
         if r.returncode == 0 or not any(m in (r.stderr or "") for m in _ADDR_IN_USE):
             return r
+        if attempt + 1 < attempts:
+            # every re-launch is visible in the test report (VERDICT r03): a
+            # failure whose stderr merely mentions the error text gets a
+            # second run, and that must not go unseen
+            tail = (r.stderr or "")[-1500:]
+            msg = (f"netutil: launch on port {port} failed with rc {r.returncode} and an "
+                   f"address-in-use message; launching again. stderr tail:\n{tail}")
+            print(msg, file=sys.stderr, flush=True)
+            warnings.warn(msg, RuntimeWarning)
     return r

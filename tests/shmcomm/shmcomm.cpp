@@ -37,8 +37,21 @@
 // the default stream, its render streams, the driver's two communication
 // streams and this library's one copy stream.  SHMCOMM_SYNC=1 (or a device without
 // stream wait-value support) selects the round-2 behaviour: each call waits
-// for its stream and completes before returning.  Never linked into the
-// product library; tests load it through the driver's rccl_path.
+// for its stream and completes before returning.
+//
+// SHMCOMM_NONBLOCKING=1 (round 4) mimics RCCL's non-blocking
+// communicators (ncclConfig_t.blocking = 0), whose calls may answer
+// ncclInProgress while they are still being set up: ncclCommInitRankConfig
+// returns at once with the join running on a helper thread; ncclAllGather,
+// ncclGroupEnd and ncclCommFinalize return ncclInProgress and are enqueued
+// (their stream event and wait recorded) a little later by a helper thread,
+// in issue order; ncclCommGetAsyncError reports ncclInProgress until that is
+// done.  A caller that records stream work behind such a call without
+// settling it first (polling ncclCommGetAsyncError) orders that work before
+// the collective -- the tests catch it as wrong data.  ncclCommAbort during
+// the join stops it.  SHMCOMM_STATS=1 prints the counts of ncclInProgress
+// answers and aborts to stderr at exit.  Never linked into the product
+// library; tests load it through the driver's rccl_path.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types and signatures only
@@ -109,6 +122,11 @@ struct Op {  // one send or receive of a group, progressed chunk by chunk
 
 struct ncclComm {
   int rank = 0, nranks = 1;
+  // non-blocking mode: creation and enqueueing state (ncclCommGetAsyncError)
+  std::atomic<int> init{ncclSuccess};     // ncclInProgress while joining
+  std::atomic<int> enqueueing{0};         // calls returned ncclInProgress, not yet enqueued
+  std::atomic<bool> abort_req{false};
+  std::thread joiner;
   std::string name;
   char* base = nullptr;
   size_t size = 0;
@@ -143,7 +161,7 @@ bool wait_for(ncclComm* c, Pred ready) {
   for (unsigned n = 0;; ++n) {
     if (ready()) return true;
     if ((n & 255) == 255) {
-      if (c->hdr()->aborted.load()) break;
+      if (c->abort_req.load() || (c->base && c->hdr()->aborted.load())) break;
       if (std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - t0).count() >
           c->timeout_ms)
         break;
@@ -398,6 +416,72 @@ void engine_drain(long timeout_ms) {
                    [&] { return E->q.empty() && !E->busy; });
 }
 
+// ---- non-blocking mode (SHMCOMM_NONBLOCKING=1) -----------------------------
+bool nonblocking_mode() {
+  const char* e = std::getenv("SHMCOMM_NONBLOCKING");
+  return e && *e && *e != '0';
+}
+std::atomic<unsigned long long> g_inprogress{0}, g_aborts{0};
+
+// One thread enqueues deferred calls in issue order, each a little later
+// (the window in which an unsettled caller would misorder its stream work).
+struct Deferred {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+};
+Deferred* deferred() {
+  static Deferred* D = [] {
+    auto* d = new Deferred;
+    std::thread([d] {
+      for (;;) {
+        std::function<void()> f;
+        {
+          std::unique_lock<std::mutex> lock(d->mu);
+          d->cv.wait(lock, [&] { return !d->q.empty(); });
+          f = std::move(d->q.front());
+          d->q.pop_front();
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(300));
+        f();
+      }
+    }).detach();
+    return d;
+  }();
+  return D;
+}
+
+// Run `enq` (which enqueues a call and returns its result) now, or -- in
+// non-blocking mode -- later on the deferred thread, answering ncclInProgress
+// until it has run (a failure then becomes the communicators' async error).
+ncclResult_t maybe_defer(const std::vector<ncclComm*>& comms, std::function<ncclResult_t()> enq) {
+  if (!nonblocking_mode()) return enq();
+  for (ncclComm* c : comms) c->enqueueing.fetch_add(1);
+  g_inprogress.fetch_add(1);
+  Deferred* D = deferred();
+  std::lock_guard<std::mutex> lock(D->mu);
+  D->q.push_back([comms, enq = std::move(enq)] {
+    const ncclResult_t rc = enq();
+    for (ncclComm* c : comms) {
+      if (rc != ncclSuccess) {
+        int expect = ncclSuccess;
+        c->async.compare_exchange_strong(expect, rc);
+      }
+      c->enqueueing.fetch_sub(1);
+    }
+  });
+  D->cv.notify_one();
+  return ncclInProgress;
+}
+
+struct StatsAtExit {
+  ~StatsAtExit() {
+    if (std::getenv("SHMCOMM_STATS"))
+      std::fprintf(stderr, "shmcomm: inprogress_returns=%llu aborts=%llu\n",
+                   (unsigned long long)g_inprogress.load(), (unsigned long long)g_aborts.load());
+  }
+} g_stats_at_exit;
+
 struct GroupEntry {
   ncclComm* comm;
   std::vector<Op> ops;
@@ -432,6 +516,10 @@ extern "C" {
 
 // 1 when calls run on the asynchronous engine, 0 when synchronously (tests)
 int shmcomm_async_engine(void) { return g_engine_state; }
+// tests: 0 ncclInProgress answers, 1 ncclCommAbort calls (this process)
+unsigned long long shmcomm_counts(int which) {
+  return which == 0 ? g_inprogress.load() : g_aborts.load();
+}
 
 ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
   if (!id) return ncclInvalidArgument;
@@ -442,9 +530,38 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
   return ncclSuccess;
 }
 
-ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int rank) {
-  if (!out || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
-  *out = nullptr;
+namespace {
+// Map the segment and wait until all ranks have joined; the communicator's
+// `init` state becomes ncclSuccess or an error.  (Blocking creation runs it
+// on the caller's thread, non-blocking creation on c->joiner.)
+ncclResult_t join(ncclComm* c, int dev) {
+  (void)hipSetDevice(dev);
+  int fd = shm_open(c->name.c_str(), O_CREAT | O_RDWR, 0600);
+  if (fd < 0 || ftruncate(fd, (off_t)c->size) != 0) {
+    if (fd >= 0) close(fd);
+    return ncclSystemError;
+  }
+  void* p = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return ncclSystemError;
+  c->base = static_cast<char*>(p);
+  // a new segment is zero-filled; the first rank to see no magic sets it
+  uint64_t expect = 0;
+  reinterpret_cast<std::atomic<uint64_t>*>(&c->hdr()->magic)
+      ->compare_exchange_strong(expect, kMagic);
+  c->hdr()->nranks = c->nranks;
+  c->copy = copy_stream();
+  // created now (its setup synchronises the device); SHMCOMM_REQUIRE_ASYNC=1
+  // makes a missing engine an error, so a test cannot pass synchronously
+  if (!engine(c->timeout_ms) && std::getenv("SHMCOMM_REQUIRE_ASYNC")) return ncclSystemError;
+  c->hdr()->joined.fetch_add(1);
+  if (!wait_for(c, [&] { return c->hdr()->joined.load() >= c->nranks; }))
+    return ncclSystemError;
+  if (c->rank == 0) shm_unlink(c->name.c_str());  // every rank has it mapped
+  return ncclSuccess;
+}
+
+ncclComm* new_comm(int nranks, const ncclUniqueId& id, int rank) {
   auto* c = new ncclComm();
   c->rank = rank;
   c->nranks = nranks;
@@ -452,76 +569,98 @@ ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int 
   if (const char* t = std::getenv("SHMCOMM_TIMEOUT_MS")) c->timeout_ms = std::atol(t);
   c->L = new Layout(nranks);
   c->size = c->L->total;
-  int fd = shm_open(c->name.c_str(), O_CREAT | O_RDWR, 0600);
-  if (fd < 0 || ftruncate(fd, (off_t)c->size) != 0) {
-    if (fd >= 0) close(fd);
-    delete c->L;
-    delete c;
-    return ncclSystemError;
-  }
-  void* p = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
-  if (p == MAP_FAILED) {
-    delete c->L;
-    delete c;
-    return ncclSystemError;
-  }
-  c->base = static_cast<char*>(p);
-  // a new segment is zero-filled; the first rank to see no magic sets it
-  uint64_t expect = 0;
-  reinterpret_cast<std::atomic<uint64_t>*>(&c->hdr()->magic)
-      ->compare_exchange_strong(expect, kMagic);
-  c->hdr()->nranks = nranks;
   c->sent.assign(nranks, 0);
   c->taken.assign(nranks, 0);
-  c->copy = copy_stream();
-  // created now (its setup synchronises the device); SHMCOMM_REQUIRE_ASYNC=1
-  // makes a missing engine an error, so a test cannot pass synchronously
-  if (!engine(c->timeout_ms) && std::getenv("SHMCOMM_REQUIRE_ASYNC")) {
-    munmap(c->base, c->size);
-    delete c->L;
-    delete c;
-    return ncclSystemError;
+  return c;
+}
+
+void free_comm(ncclComm* c) {
+  if (c->joiner.joinable()) c->joiner.join();
+  if (c->base) munmap(c->base, c->size);
+  delete c->L;
+  delete c;
+}
+}  // namespace
+
+ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqueId id, int rank) {
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+  *out = nullptr;
+  ncclComm* c = new_comm(nranks, id, rank);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const ncclResult_t rc = join(c, dev);
+  if (rc != ncclSuccess) {
+    free_comm(c);
+    return rc;
   }
-  c->hdr()->joined.fetch_add(1);
-  if (!wait_for(c, [&] { return c->hdr()->joined.load() >= nranks; })) {
-    munmap(c->base, c->size);
-    delete c->L;
-    delete c;
-    return ncclSystemError;
-  }
-  if (rank == 0) shm_unlink(c->name.c_str());  // every rank has it mapped
   *out = c;
   return ncclSuccess;
 }
 
-// The driver creates communicators through this entry point when it exists
-// (non-blocking, polled with ncclCommGetAsyncError): here creation completes
-// before returning, so the state it polls is ncclSuccess at once.
+// The driver creates communicators through this entry point when it exists,
+// non-blocking (config->blocking = 0), and polls ncclCommGetAsyncError.  By
+// default creation completes before returning, so the state it polls is
+// ncclSuccess at once; with SHMCOMM_NONBLOCKING=1 the join runs on a helper
+// thread and the call answers ncclInProgress, as RCCL does.
 ncclResult_t ncclCommInitRankConfig(ncclComm_t* out, int nranks, ncclUniqueId id, int rank,
-                                    ncclConfig_t*) {
-  return ncclCommInitRank(out, nranks, id, rank);
+                                    ncclConfig_t* config) {
+  if (!(nonblocking_mode() && config && config->blocking == 0))
+    return ncclCommInitRank(out, nranks, id, rank);
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+  ncclComm* c = new_comm(nranks, id, rank);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  c->init.store(ncclInProgress);
+  c->joiner = std::thread([c, dev] { c->init.store(join(c, dev)); });
+  *out = c;
+  g_inprogress.fetch_add(1);
+  return ncclInProgress;
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t c) {
   if (!c) return ncclSuccess;
-  engine_drain(c->timeout_ms);   // no call of it still running
+  if (c->joiner.joinable()) {   // a non-blocking creation still joining: stop it
+    c->abort_req.store(true);
+    c->joiner.join();
+  }
+  if (c->init.load() == ncclSuccess) engine_drain(c->timeout_ms);   // no call of it still running
   // (the copy stream is the process's, shared by its communicators)
-  munmap(c->base, c->size);
-  delete c->L;
-  delete c;
+  free_comm(c);
   return ncclSuccess;
 }
 
 ncclResult_t ncclCommAbort(ncclComm_t c) {
   if (!c) return ncclSuccess;
-  c->hdr()->aborted.store(1);  // peers' waits end with an error
+  g_aborts.fetch_add(1);
+  c->abort_req.store(true);
+  if (c->joiner.joinable()) c->joiner.join();
+  if (c->base) c->hdr()->aborted.store(1);   // peers' waits end with an error
+  if (c->init.load() != ncclSuccess) shm_unlink(c->name.c_str());   // nobody else will
   return ncclCommDestroy(c);
+}
+
+// Non-blocking mode: flushes the communicator's calls (engine drain) on the
+// deferred thread, answering ncclInProgress meanwhile.
+ncclResult_t ncclCommFinalize(ncclComm_t c) {
+  if (!c) return ncclInvalidArgument;
+  if (!nonblocking_mode()) return ncclSuccess;
+  const long t = c->timeout_ms;
+  return maybe_defer({c}, [t] {
+    engine_drain(t);
+    return ncclSuccess;
+  });
 }
 
 ncclResult_t ncclCommGetAsyncError(ncclComm_t c, ncclResult_t* e) {
   if (!c || !e) return ncclInvalidArgument;
-  *e = c->hdr()->aborted.load() ? ncclRemoteError : (ncclResult_t)c->async.load();
+  const int init = c->init.load();
+  if (init != ncclSuccess) {
+    *e = (ncclResult_t)init;
+    return ncclSuccess;
+  }
+  if (c->hdr()->aborted.load()) *e = ncclRemoteError;
+  else if (c->async.load() != ncclSuccess) *e = (ncclResult_t)c->async.load();
+  else *e = c->enqueueing.load() > 0 ? ncclInProgress : ncclSuccess;
   return ncclSuccess;
 }
 
@@ -531,7 +670,7 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t count,
   const size_t bytes = count * dtype_size(datatype);
   if (bytes > kAgBytes) return ncclInvalidArgument;
   const uint64_t k = c->ag_ops++;   // issue order = the engine's order
-  return submit({stream}, {c}, [c, k, bytes, sendbuff, recvbuff]() -> ncclResult_t {
+  return maybe_defer({c}, [=] { return submit({stream}, {c}, [c, k, bytes, sendbuff, recvbuff]() -> ncclResult_t {
     const int slot = int(k % kAgSlots);
     // the slot is free once every rank has finished all-gather k - kAgSlots
     if (!wait_for(c, [&] {
@@ -553,7 +692,7 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t count,
     }
     c->ag(c->rank)->done.store(k + 1, std::memory_order_release);
     return ncclSuccess;
-  });
+  }); });
 }
 
 ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
@@ -591,13 +730,15 @@ ncclResult_t ncclGroupEnd() {
     }
   }
   auto shared = std::make_shared<std::vector<GroupEntry>>(std::move(groups));
-  return submit(streams, comms, [shared]() {
-    ncclResult_t rc = ncclSuccess;
-    for (auto& g : *shared) {
-      const ncclResult_t r = run_ops(g.comm, g.ops);
-      if (rc == ncclSuccess) rc = r;
-    }
-    return rc;
+  return maybe_defer(comms, [=] {
+    return submit(streams, comms, [shared]() {
+      ncclResult_t rc = ncclSuccess;
+      for (auto& g : *shared) {
+        const ncclResult_t r = run_ops(g.comm, g.ops);
+        if (rc == ncclSuccess) rc = r;
+      }
+      return rc;
+    });
   });
 }
 

@@ -9,8 +9,13 @@ cr_math.h), checked EXHAUSTIVELY on the GPU by tests/crmath/crmath_check.hip:
     cr_logf (oracle/sdf_oracle.c), the Mandelbulb DE's log -- for all 2^32
     inputs;
   * the smooth-min's h = n / k by div_scaled: its bits equal IEEE n / k, or
-    (only where h < 2^-78) h*h*k/4 does, over 2^32 (k, n) pairs with k
-    log-uniform over every positive exponent and n over [0, k].
+    (only where h < 2^-78) h*h*k/4 does, over 2^32 SAMPLED (k, n) pairs with
+    k log-uniform over every positive exponent and n over [0, k], and over
+    2^32 more from its edge families (denormal k, k near FLT_MAX, n * sc
+    underflowing, tiny normal k) -- its proof is Markstein's theorem;
+  * shade.h spec_pow (exact precision's x^n by repeated squaring in fp64) is
+    bit-identical to the library (float)pow((double)x, n) for every float x
+    in [0, 1.0001] and every integer n in [0, 64].
 
 With those, the exact-precision kernel stays bit-exact with the oracle
 (test_gpu_parity.py's full-size exact cases)."""
@@ -59,3 +64,13 @@ def test_cr_log_is_the_oracles_log_everywhere(results):
 def test_smooth_min_division_is_bit_identical_where_it_counts(results):
     r = results["smin"]
     assert r["effective"] == 0, r
+
+
+def test_smooth_min_division_edge_families(results):
+    r = results["sminedge"]
+    assert r["inputs"] == 2**32 and r["effective"] == 0, r
+
+
+def test_integer_pow_is_the_library_pow(results):
+    r = results["pow"]
+    assert r["inputs"] == 0x3F800347 and r["mismatch"] == 0, r

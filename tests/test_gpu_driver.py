@@ -128,9 +128,10 @@ def test_frame_not_shipped_is_refused(nccl_world1):
     assert torch.equal(got.view(torch.int32), _reference(f).view(torch.int32))
 
 
-@pytest.mark.parametrize("nproc,cfg,shares", [(2, "C3", None), (3, "C3", "1:2"), (8, "C3", None),
-                                              (8, "C4", None)])
-def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
+@pytest.mark.parametrize("nproc,cfg,shares,batch,streams,nonblocking", [
+    (2, "C3", None, 2, 4, True), (3, "C3", "1:2", 1, 4, False), (8, "C3", None, 4, 8, True),
+    (8, "C4", None, 0, 0, False)])
+def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, nonblocking):
     """The native C++ driver's multi-rank sequence (render, RCCL-style length
     all-gather, send/recv of the TILES streams to rank 0, decode) with
     `nproc` ranks sharing this GPU: bench.py --driver native over the
@@ -140,7 +141,13 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
     place, and one FIFO engine per rank makes any cross-communicator order
     mismatch between ranks an error.  Rank 0's assembled last frame must equal a single-device
     render bit for bit; the 8-rank C4 case is the round-end N = 8 bench's
-    configuration (4K, default 2:7 shares)."""
+    configuration (4K, default 2:7 shares, batches of 2 frames).  Frames
+    are shipped in batches (1, 2, 4: one length all-gather and one send/recv
+    group per batch; the warm-up's drain closes a short batch, so the next
+    batch starts on a new buffer set).  `nonblocking`: the stand-in answers
+    ncclInProgress for creation, all-gathers and groups (as RCCL's
+    non-blocking communicators may) and enqueues them later, so work the
+    driver recorded behind an unsettled call would run before it."""
     import json
     import sys
     assert SHMCOMM.exists(), "build() must produce tests/shmcomm/libshmcomm.so"
@@ -152,17 +159,29 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares):
              str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "6", "--warmup", "2",
              "--backend", "gloo", "--comm-lib", str(SHMCOMM), "--driver", "native",
              "--config", cfg, "--no-display", "--clock-warm-s", "0"]
+        c += ["--batch", str(batch)] if batch else []
+        c += ["--streams", str(streams)] if streams else []
         return c + (["--shares", shares] if shares else [])
     env = dict(os.environ, SHMCOMM_TIMEOUT_MS="60000", GPU_MAX_HW_QUEUES="8",
-                   SHMCOMM_REQUIRE_ASYNC="1")
+               SHMCOMM_REQUIRE_ASYNC="1", SHMCOMM_STATS="1")
+    if nonblocking:
+        env["SHMCOMM_NONBLOCKING"] = "1"
     r = run_launcher(cmd, timeout=400, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == nproc and d["frame_verified"] is True, d
     assert d["config"]["driver"].startswith("native"), d["config"]
     assert d["config"]["wire"] == "tiles"
+    assert d["config"]["batch"] == (batch or 2), d["config"]
     if nproc == 8:
         assert d["config"]["tiling"].startswith("8-row blocks, rank 0 2 / others 7")
+    import re
+    counts = [int(m) for m in re.findall(r"shmcomm: inprogress_returns=(\d+)", r.stderr)]
+    assert len(counts) >= nproc, r.stderr[-2000:]
+    if nonblocking:   # every rank's creations, all-gathers and groups answered "in progress"
+        assert min(counts) > 2, counts
+    else:
+        assert max(counts) == 0, counts
 
 
 def _read_ppm(path):

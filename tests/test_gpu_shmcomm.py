@@ -43,3 +43,19 @@ def test_crossed_communicator_order_is_an_error_not_a_hang(tmp_path):
     assert any(e != 0 for r in res for e in r["async_errors"]), res
     for r in res:
         assert r["drain_s"] < 60, r     # the streams were released
+
+
+def test_nonblocking_creation_timeout_aborts(tmp_path):
+    """sdf_comm_create over a non-blocking communicator
+    (ncclCommInitRankConfig answers ncclInProgress) whose peer never joins
+    gives SDF_E_TIMEOUT after its limit and aborts the half-made
+    communicator (no join left running, no handle returned)."""
+    env = dict(os.environ, SHMCOMM_NONBLOCKING="1", SHMCOMM_TIMEOUT_MS="60000",
+               GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, str(HERE / "shmcomm" / "create_probe.py"), "1500"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["rc"] == -6 and d["handle_null"], d            # SDF_E_TIMEOUT
+    assert d["inprogress_returns"] >= 1 and d["aborts"] == 1, d
+    assert 1.4 < d["seconds"] < 30, d
