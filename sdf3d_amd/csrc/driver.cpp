@@ -45,6 +45,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -188,8 +190,27 @@ struct sdf_driver {
 
 namespace {
 
-int hip_ok(hipError_t e) { return e == hipSuccess ? SDF_OK : SDF_E_HIP; }
-int nccl_ok(ncclResult_t e) { return e == ncclSuccess ? SDF_OK : SDF_E_COMM; }
+// SDF3D_DRIVER_DEBUG=1: every failed HIP / RCCL call is reported on stderr
+// with its source line and error (diagnosis of multi-rank runs)
+bool debug_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SDF3D_DRIVER_DEBUG");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+int hip_ok(hipError_t e, int line = __builtin_LINE()) {
+  if (e == hipSuccess) return SDF_OK;
+  if (debug_on())
+    std::fprintf(stderr, "sdf driver: HIP error %d (%s) at driver.cpp:%d\n", (int)e,
+                 hipGetErrorString(e), line);
+  return SDF_E_HIP;
+}
+int nccl_ok(ncclResult_t e, int line = __builtin_LINE()) {
+  if (e == ncclSuccess) return SDF_OK;
+  if (debug_on()) std::fprintf(stderr, "sdf driver: RCCL error %d at driver.cpp:%d\n", (int)e, line);
+  return SDF_E_COMM;
+}
 
 // A communicator created non-blocking (sdf_comm_create) may answer any call
 // with ncclInProgress while RCCL finishes it in the background; the next call
@@ -684,6 +705,9 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
   if (d->sender) rc = sdf::launch_render_plan(d->plan_send[b], s);
   if (rc == SDF_OK && d->root && !d->sender) rc = sdf::launch_render_plan(d->plan_frame[b], s);
   d->t_render += seconds_since(tr);
+  if (rc != SDF_OK && debug_on())
+    std::fprintf(stderr, "sdf driver: render launch failed (%d): %s\n", rc,
+                 hipGetErrorString(hipGetLastError()));
   if (rc != SDF_OK) return fail(d, rc);
   if (frame_index) *frame_index = i;
   d->next = i + 1;

@@ -12,6 +12,8 @@
 //          (ADVICE r03): denormal k; k within 2^20 ulps of FLT_MAX; k >= 2^64
 //          with n so small that n * sc underflows; tiny normal k (2^-126 ..
 //          2^-100)
+//   minmax : v_min_f32 / v_max_f32 vs the GLSL select on the operand pairs
+//          the exact kernel relies on (hw_min / hw_max)
 //   pow  : shade.h spec_pow<exact>(x, n) (repeated squaring in fp64, the
 //          library pow on lanes near a rounding boundary) vs the library
 //          (float)pow((double)x, (double)n), for EVERY float x in [0, 1.0001]
@@ -151,6 +153,44 @@ __global__ void check_smin_edges(unsigned base, Counts* c) {
   smin_case(k, n, i, c);
 }
 
+// The hardware v_min_f32 / v_max_f32 against the GLSL select gmin/gmax on
+// the operand pairs where the exact kernel uses the former (render_kernel.inc
+// hw_min / hw_max): the select returns its first operand unless the second
+// is strictly smaller (larger), so the two differ only for a NaN first
+// operand or a (+0, -0) / (-0, +0) pair.  Lane i takes pair i of the table.
+__device__ __forceinline__ float hwmin(float x, float y) {
+  float r;
+  asm volatile("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__device__ __forceinline__ float hwmax(float x, float y) {
+  float r;
+  asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+__global__ void check_minmax(unsigned base, Counts* c) {
+  const unsigned i = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const float nan = __uint_as_float(0x7FC00000u), inf = __builtin_inff();
+  const float z = 0.0f, nz = __uint_as_float(0x80000000u);
+  // min(x, y): (accumulator or shadow value, primitive value or quotient)
+  const float mins[][2] = {{nz, z}, {z, 1.0f}, {1.0f, z}, {-1.0f, 2.0f}, {2.0f, -1.0f},
+                           {1.0f, nan}, {-inf, nan}, {z, nan}, {nz, nan}, {inf, 3.0f},
+                           {nz, 1.0f}, {z, inf}, {-3.0f, -3.0f}};
+  // max(x, +0) / max(+0, y): the smooth-min's h, the shadow's denominator
+  const float maxs[][2] = {{z, z}, {1.0f, z}, {-1.0f, z}, {-inf, z}, {inf, z},
+                           {z, nan}, {z, -1.0f}, {z, 2.0f}, {z, -inf}};
+  constexpr unsigned nmin = sizeof(mins) / sizeof(mins[0]), nmax = sizeof(maxs) / sizeof(maxs[0]);
+  bool bad = false;
+  if (i < nmin) {
+    const float x = mins[i][0], y = mins[i][1];
+    bad = !same_bits(hwmin(x, y), y < x ? y : x);
+  } else if (i < nmin + nmax) {
+    const float x = maxs[i - nmin][0], y = maxs[i - nmin][1];
+    bad = !same_bits(hwmax(x, y), x < y ? y : x);
+  }
+  if (i < nmin + nmax) tally(c, bad, true, bad, i);
+}
+
 // x = index (bits) in [0, 0x3F800347) i.e. [0, 1.0001]; every n in [0, 64]
 constexpr unsigned kPowXEnd = 0x3F800347u;
 __global__ void check_pow(unsigned base, Counts* c) {
@@ -201,7 +241,7 @@ int main(int argc, char** argv) {
   } checks[] = {{"rcp", check_rcp, 1ull << 32, ""},   {"sqrt", check_sqrt, 1ull << 32, ""},
                 {"log", check_log, 1ull << 32, ""},   {"smin", check_smin, 1ull << 32, ""},
                 {"sminedge", check_smin_edges, 1ull << 32, ""},
-                {"pow", check_pow, kPowXEnd, ""}};
+                {"pow", check_pow, kPowXEnd, ""}, {"minmax", check_minmax, 256, ""}};
   // an argument selects checks by name (e.g. "sqrt,log"; "smin" matches only
   // itself)
   auto wanted = [&](const char* name) {

@@ -59,6 +59,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -245,15 +246,29 @@ bool progress(ncclComm* c, Op& op) {
   return moved;
 }
 
+// Several ops of a group between the same pair of ranks in the same
+// direction share one channel, so they are matched in issue order (as RCCL
+// matches point-to-point calls): an op moves only after every earlier op of
+// its channel has finished.  (Progressing them independently let a later
+// receive take a chunk an earlier one had just missed -- a data race that
+// batched ships, several frames per peer in one group, turned into a decode
+// of a mixed-up stream.)
 ncclResult_t run_ops(ncclComm* c, std::vector<Op>& ops) {
   for (Op& op : ops) op.nchunks = (op.bytes + kChunk - 1) / kChunk;
   bool all = false;
+  std::vector<char> busy(2 * size_t(c->nranks));   // (peer, direction) has an unfinished earlier op
   auto finished = [&] {
     all = true;
+    std::fill(busy.begin(), busy.end(), 0);
     for (Op& op : ops) {
-      progress(c, op);
+      if (op.chunk == op.nchunks) continue;
+      char& b = busy[2 * size_t(op.peer) + (op.send ? 1 : 0)];
+      if (!b) progress(c, op);
       if (c->async.load() != ncclSuccess) return true;
-      all = all && op.chunk == op.nchunks;
+      if (op.chunk != op.nchunks) {
+        b = 1;
+        all = false;
+      }
     }
     return all;
   };

@@ -74,3 +74,11 @@ def test_smooth_min_division_edge_families(results):
 def test_integer_pow_is_the_library_pow(results):
     r = results["pow"]
     assert r["inputs"] == 0x3F800347 and r["mismatch"] == 0, r
+
+
+def test_hardware_min_max_equal_the_select_where_used(results):
+    """render_kernel.inc hw_min / hw_max (exact precision) replace the GLSL
+    select only where the operands make them equal; the signed-zero and NaN
+    pairs those proofs rest on are checked on the hardware."""
+    r = results["minmax"]
+    assert r["mismatch"] == 0 and r["fast_path"] == 22, r

@@ -129,8 +129,8 @@ def test_frame_not_shipped_is_refused(nccl_world1):
 
 
 @pytest.mark.parametrize("nproc,cfg,shares,batch,streams,nonblocking", [
-    (2, "C3", None, 2, 4, True), (3, "C3", "1:2", 1, 4, False), (8, "C3", None, 4, 8, True),
-    (8, "C4", None, 0, 0, False)])
+    (2, "C3", None, 2, 4, True), (3, "C3", "1:2", 1, 4, False), (3, "C3", None, 4, 8, True),
+    (8, "C3", None, 4, 8, False), (8, "C4", None, 0, 0, False)])
 def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, nonblocking):
     """The native C++ driver's multi-rank sequence (render, RCCL-style length
     all-gather, send/recv of the TILES streams to rank 0, decode) with
@@ -155,7 +155,7 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, n
 
     def cmd(port):
         c = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-             str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
+             str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port), "--tee", "2",
              str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "6", "--warmup", "2",
              "--backend", "gloo", "--comm-lib", str(SHMCOMM), "--driver", "native",
              "--config", cfg, "--no-display", "--clock-warm-s", "0"]
@@ -167,7 +167,12 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, n
     if nonblocking:
         env["SHMCOMM_NONBLOCKING"] = "1"
     r = run_launcher(cmd, timeout=400, cwd=ROOT, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
+    if r.returncode != 0:   # the ranks' own error lines first (torchrun's summary is long)
+        import re
+        bad = [l for l in (r.stderr or "").splitlines()
+               if re.search(r"terminate|what\(\)|Error|error|Assert|abort|SIG", l)
+               and "error_file" not in l]
+        raise AssertionError("\n".join(bad[:60]) + "\n----\n" + r.stderr[-3000:])
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == nproc and d["frame_verified"] is True, d
     assert d["config"]["driver"].startswith("native"), d["config"]
