@@ -624,6 +624,10 @@ def main():
             # host (CPU) time of the frame loop's own calls per frame, waits
             # for the GPU / peers excluded (native driver only)
             "driver_host_us_per_frame": drv.stats()["host_us_per_frame"] if native else None,
+            # the same split by the driver's enqueue calls (renders with the
+            # TILES compaction, length all-gathers, send/recv groups, decodes)
+            "driver_enqueue_us_per_frame": (drv.stats()["enqueue_us_per_frame"] if native
+                                            else None),
         }
         pmc = (pmc_summary(args.config, args.precision)
                if world == 1 and args.format == "rgba32f" else {})

@@ -27,6 +27,7 @@ d = json.loads([l for l in open(f"gpurun_out/host_probe_b{b}.json") if l.startsw
 print(json.dumps({"batch": int(b), "world": d["n_gpus"], "config": d["config"]["workload"][:3],
                   "streams": d["config"]["streams"], "lag": d["config"]["lag"],
                   "driver_host_us_per_frame": d["driver_host_us_per_frame"],
+                  "driver_enqueue_us_per_frame": d.get("driver_enqueue_us_per_frame"),
                   "ms_per_step": d["ms_per_step"], "frame_verified": d["frame_verified"]}))
 PY
   tail -1 gpurun_out/host_probe.jsonl

@@ -3,8 +3,9 @@
 # row shares (tools/root_probe.py), one JSON per run in gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
-for spec in ${SPECS:-"8 1:2" "8 1:3" "8 1:4" "8 2:7" "4 1:1" "4 3:4" "4 2:3" "2 1:1" "2 4:3"}; do
-  set -- $spec
+# SPECS: "N,a:b ..." (default: the candidate shares at N = 8, 4, 2)
+for spec in ${SPECS:-8,1:2 8,1:3 8,1:4 8,2:7 4,1:1 4,3:4 4,2:3 2,1:1 2,4:3}; do
+  set -- ${spec/,/ }
   out="gpurun_out/rp$1_${2/:/-}.json"
   timeout -k 10 200 python tools/root_probe.py --world $1 --shares $2 --frames 400 > "$out" 2>> gpurun_out/rp.log
   rc=$?; [ $rc -eq 0 ] || { echo "N=$1 $2 rc=$rc"; exit $rc; }
