@@ -67,6 +67,18 @@ struct KernelArgs {
   int32_t* steps;       // rows * width int2 or null
 };
 
+// Waves (8x8 tiles side by side) per render workgroup (render_kernel.inc
+// render / render_tiles; the built-in and the run-time specialised launchers).
+// Round 4: one wave per workgroup -- each wave is placed on its own, so the
+// frame's last, longest tiles pack onto the CUs better than in 4-wave groups
+// that need four slots of one CU: C4 fast 0-1.6 % faster, C5 fast up to 4 %,
+// C4/C5 exact 0.2-1.8 % (profiles/r04_ab_workgroup.json; 2 waves lie between,
+// 8 are 3-5 % slower).  Overridable for experiments (SDF_WG_WAVES).
+#ifndef SDF_WG_WAVES
+#define SDF_WG_WAVES 1
+#endif
+constexpr int kWgWaves = SDF_WG_WAVES;
+
 // ---- frame sequences (sdf_render_frames) ----------------------------------
 // Up to kFramesPerLaunch whole frames of one scene in one launch of a
 // persistent kernel: its waves take 8x8 tiles of all the launch's frames from
