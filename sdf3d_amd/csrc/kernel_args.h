@@ -127,6 +127,13 @@ int launch_render_fast(const KernelArgs& a, int variant, void* stream);
 // the persistent frame-sequence kernel on `nblocks` 256-thread workgroups
 int launch_frames_exact(const FramesArgs& a, int variant, int nblocks, void* stream);
 int launch_frames_fast(const FramesArgs& a, int variant, int nblocks, void* stream);
+// the Mandelbulb scene's kernels live in units of their own
+// (render_{fast,exact}_bulb.hip, scheduled for ILP: sdf3d_amd/build.py); the
+// launchers above forward kVariantBulb to these
+int launch_render_exact_bulb(const KernelArgs& a, void* stream);
+int launch_render_fast_bulb(const KernelArgs& a, void* stream);
+int launch_frames_exact_bulb(const FramesArgs& a, int nblocks, void* stream);
+int launch_frames_fast_bulb(const FramesArgs& a, int nblocks, void* stream);
 int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int row_bytes,
                         int height, int block_rows, void* frame, void* stream);
 int launch_heatmap(const int32_t* steps, int count, int which, int max_steps, int format,

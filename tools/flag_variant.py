@@ -28,7 +28,7 @@ def main():
     out.mkdir(parents=True, exist_ok=True)
     objs = []
     for src, extra in b.UNITS:
-        if src in ("render_fast.hip", "render_exact.hip"):
+        if src.startswith("render_"):
             o = out / (Path(src).stem + ".o")
             subprocess.run([b._hipcc(), *b.COMMON, *extra, *flags, "-I", str(b.OBJ), "-c",
                             str(b.CSRC / src), "-o", str(o)], check=True)
