@@ -24,7 +24,7 @@ for s in $STEPS; do
       done ;;
     configs)
       : > gpurun_out/configs.jsonl
-      for spec in "C4 fast" "C4 exact" "C3 fast" "C2 fast" "C5 fast" "C5 exact" "C1 fast"; do
+      for spec in ${CONFIG_SPECS:-"C4 fast" "C4 exact" "C3 fast" "C3 exact" "C2 fast" "C5 fast" "C5 exact" "C1 fast"}; do
         set -- $spec
         timeout -k 10 300 python bench.py --config $1 --precision $2 --steps 30 --warmup 3 \
           --no-cpu-baseline --no-display --no-exact >> gpurun_out/configs.jsonl 2>> gpurun_out/configs.log
