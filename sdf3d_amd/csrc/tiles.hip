@@ -63,8 +63,24 @@ __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
 }
 
 // tiles per wave of the decoder: 4 (0.051 ms for the root's 7/8 of a 4K
-// frame) beats 2 (0.055); forcing 8 waves / SIMD spills and gains nothing
-constexpr int kDecodeTiles = 4;
+// frame) beats 2 (0.055); forcing 8 waves / SIMD spills and gains nothing.
+// Round 4 (rank 0's 49/51 of the 4K C4 frame, profiles/r04_decode_ab.json):
+// non-temporal frame stores 0.0445 against 0.0466 ms; one-wave workgroups
+// 0.0470 (four kept); the column scan and the 16- and 8-bit transpose stages
+// on the VALU (v_permlane16/32_swap, v_perm_b32, DPP row_ror) instead of
+// ds_bpermute / ds_swizzle 0.0506 (not kept: the LDS round trips were not
+// what bounds it, the extra VALU work and hazard waits are).
+#ifndef SDF_DECODE_TILES
+#define SDF_DECODE_TILES 4
+#endif
+#ifndef SDF_DECODE_WG_WAVES
+#define SDF_DECODE_WG_WAVES 4   // waves per decoder workgroup
+#endif
+#ifndef SDF_DECODE_NT
+#define SDF_DECODE_NT 1         // the frame's pixels by non-temporal stores
+#endif
+constexpr int kDecodeTiles = SDF_DECODE_TILES;
+constexpr int kDecodeWgWaves = SDF_DECODE_WG_WAVES;
 
 // One wave = TPW consecutive tiles of one part, lane j = pixel (j / 8, j % 8)
 // of each.  The memory traffic is issued up front in two dependent rounds:
@@ -80,7 +96,7 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
   // the wave index as a scalar: from threadIdx.x the compiler cannot tell it
   // is wave-uniform and would run all tile / part arithmetic (divisions
   // included) on the VALU
-  const int gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gw = blockIdx.x * kDecodeWgWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int part = gw / waves_per_part;
   if (part >= D.nparts) return;
   const int tbase = (gw - part * waves_per_part) * TPW;
@@ -250,66 +266,72 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
       float4 px = make_float4(v[0], v[1], v[2], 1.0f);
       if (shade == kTilesShadeFast) px = shade_colour<false>(K, v[0], v[1], v[2]);
       else if (shade == kTilesShadeExact) px = shade_colour<true>(K, v[0], v[1], v[2]);
-      frame[(size_t)y * width + x] = px;
+      if constexpr (SDF_DECODE_NT) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f pv = {px.x, px.y, px.z, px.w};
+        __builtin_nontemporal_store(pv, reinterpret_cast<v4f*>(frame + (size_t)y * width + x));
+      } else {
+        frame[(size_t)y * width + x] = px;
+      }
     }
     (void)nq;
   }
 }
 
-__global__ __launch_bounds__(256) void decode_tiles(const DecodeParts D,
+__global__ __launch_bounds__(64 * kDecodeWgWaves) void decode_tiles(const DecodeParts D,
                                                     const uint8_t* __restrict__ parts,
                                                     int waves_per_part, float4* __restrict__ frame) {
   decode_body<kDecodeTiles>(D, parts, waves_per_part, frame);
 }
 
 // Offsets of the plane blocks in tile order: exclusive scan of 8 * (w0 + w1
-// + w2) over the heads.  tiles_scan: 256 threads x 8 consecutive tiles per
-// block of kScanTiles -> block-local offsets + the block's total.
+// + w2) over the heads.  tiles_scan: one wave x 32 consecutive tiles per lane
+// per block of kScanTiles -> block-local offsets + the block's total.
 // tiles_move: one wave per 8 consecutive tiles (in one scan block) adds the
 // block's prefix (the sum of earlier block totals, a wave reduction), writes
 // the final offsets and copies the tiles' planes from their slots into the
 // stream, the 8 tiles' loads in flight together (one wave per tile took
-// 30.7 us on a whole 4K frame); the last tile writes `used`.
+// 30.7 us on a whole 4K frame); the last tile writes `used`.  Both launch
+// one-wave workgroups (round 4): they run beside the next frames' render
+// kernels, whose one-wave workgroups fill the CUs, and a wave finds a free
+// slot long before four waves on one CU do.
 __device__ __forceinline__ uint32_t plane_bytes(uint32_t head) { return 8u * tile_qwords(head); }
 
-__global__ __launch_bounds__(256) void tiles_scan(uint8_t* buf, int ntiles) {
+constexpr int kScanLaneTiles = kScanTiles / 64;   // consecutive tiles per lane
+
+__global__ __launch_bounds__(64) void tiles_scan(uint8_t* buf, int ntiles) {
   const TilesLayout L(ntiles);
   const uint4* head = reinterpret_cast<const uint4*>(buf + L.head);
   uint32_t* table = reinterpret_cast<uint32_t*>(buf + L.table);
-  __shared__ uint32_t wsum[4];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int t0 = blockIdx.x * kScanTiles + tid * 8;
-  uint32_t sz[8], sum = 0;
+  const int lane = threadIdx.x;
+  const int t0 = blockIdx.x * kScanTiles + lane * kScanLaneTiles;
+  uint32_t sz[kScanLaneTiles], sum = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < kScanLaneTiles; i++) {
     sz[i] = t0 + i < ntiles ? plane_bytes(head[t0 + i].x) : 0u;
     sum += sz[i];
   }
-  // block exclusive scan of the thread sums: wave scan, then wave totals
+  // exclusive scan of the lane sums
   uint32_t inc = sum;
 #pragma unroll
   for (int s = 1; s < 64; s <<= 1) {
     const uint32_t v = (uint32_t)__shfl_up((int)inc, s, 64);
     if (lane >= s) inc += v;
   }
-  if (lane == 63) wsum[wv] = inc;
-  __syncthreads();
   uint32_t off = inc - sum;
-  for (int i = 0; i < wv; i++) off += wsum[i];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < kScanLaneTiles; i++) {
     if (t0 + i < ntiles) table[t0 + i] = off;
     off += sz[i];
   }
-  if (tid == 255)
-    reinterpret_cast<uint32_t*>(buf + L.bsums)[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (lane == 63) reinterpret_cast<uint32_t*>(buf + L.bsums)[blockIdx.x] = inc;
 }
 
 constexpr int kMoveTiles = 8;   // tiles per wave of tiles_move (divides kScanTiles)
 
-__global__ __launch_bounds__(256) void tiles_move(uint8_t* buf, int ntiles, uint32_t* used_out) {
+__global__ __launch_bounds__(64) void tiles_move(uint8_t* buf, int ntiles, uint32_t* used_out) {
   const TilesLayout L(ntiles);
-  const int t0 = (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * kMoveTiles;
+  const int t0 = blockIdx.x * kMoveTiles;
   if (t0 >= ntiles) return;
   const int lane = threadIdx.x & 63;
   const int nt = min(kMoveTiles, ntiles - t0);
@@ -359,11 +381,11 @@ int launch_tiles_compact(void* stream_buf, int ntiles, void* stream, uint32_t* u
   if (ntiles <= 0) return 0;
   (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
   uint8_t* buf = reinterpret_cast<uint8_t*>(stream_buf);
-  hipLaunchKernelGGL(tiles_scan, dim3((ntiles + kScanTiles - 1) / kScanTiles), dim3(256), 0,
+  hipLaunchKernelGGL(tiles_scan, dim3((ntiles + kScanTiles - 1) / kScanTiles), dim3(64), 0,
                      (hipStream_t)stream, buf, ntiles);
   const int waves = (ntiles + kMoveTiles - 1) / kMoveTiles;
-  hipLaunchKernelGGL(tiles_move, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, buf,
-                     ntiles, used_out);
+  hipLaunchKernelGGL(tiles_move, dim3(waves), dim3(64), 0, (hipStream_t)stream, buf, ntiles,
+                     used_out);
   return (int)hipGetLastError();
 }
 
@@ -376,7 +398,8 @@ int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, vo
   const long long waves = (long long)waves_per_part * d.nparts;
   if (waves == 0) return 0;
   (void)hipGetLastError();  // a stale error of an earlier call is not this launch's
-  hipLaunchKernelGGL(decode_tiles, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(decode_tiles, dim3((unsigned)((waves + kDecodeWgWaves - 1) / kDecodeWgWaves)),
+                     dim3(64 * kDecodeWgWaves), 0,
                      (hipStream_t)stream, d, reinterpret_cast<const uint8_t*>(parts),
                      waves_per_part, reinterpret_cast<float4*>(frame));
   return (int)hipGetLastError();

@@ -3,10 +3,11 @@
 flags on the render translation units (kernel A/B experiments), side by side
 for tools/ab_kernel.py:
 
-    python tools/flag_variant.py NAME [-DFLAG=1 ...]   -> tools/_variants/libsdf3d_NAME.so
+    python tools/flag_variant.py NAME [--units=tiles] [-DFLAG=1 ...]
+        -> tools/_variants/libsdf3d_NAME.so
 
-The render units (render_fast.hip, render_exact.hip) are compiled with the
-flags into tools/_variants/NAME/; every other object is the in-tree build's
+The units whose names start with one of --units (default: render_, the
+render units) are compiled with the flags into tools/_variants/NAME/; every other object is the in-tree build's
 (sdf3d_amd/build/*.o, built first).  Variants of several names build in
 parallel when run as separate processes.
 """
@@ -22,13 +23,17 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     name, flags = sys.argv[1], sys.argv[2:]
+    prefixes = ("render_",)
+    if flags and flags[0].startswith("--units="):
+        prefixes = tuple(flags[0].split("=", 1)[1].split(","))
+        flags = flags[1:]
     from sdf3d_amd import build as b
     b.build_library(verbose=False)
     out = ROOT / "tools" / "_variants" / name
     out.mkdir(parents=True, exist_ok=True)
     objs = []
     for src, extra in b.UNITS:
-        if src.startswith("render_"):
+        if src.startswith(prefixes):
             o = out / (Path(src).stem + ".o")
             subprocess.run([b._hipcc(), *b.COMMON, *extra, *flags, "-I", str(b.OBJ), "-c",
                             str(b.CSRC / src), "-o", str(o)], check=True)
