@@ -79,6 +79,12 @@ __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
 #ifndef SDF_DECODE_NT
 #define SDF_DECODE_NT 1         // the frame's pixels by non-temporal stores
 #endif
+#ifndef SDF_DECODE_ESC_VMEM
+#define SDF_DECODE_ESC_VMEM 0   // 1: a pixel's escape window by its own loads, not ds_bpermute
+#endif
+#ifndef SDF_DECODE_SKIP
+#define SDF_DECODE_SKIP 0   // timing probes only (wrong pixels): 1 transpose, 2 escapes, 4 scan, 8 shade
+#endif
 constexpr int kDecodeTiles = SDF_DECODE_TILES;
 constexpr int kDecodeWgWaves = SDF_DECODE_WG_WAVES;
 
@@ -175,7 +181,7 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
     const int B = bw[0] + bw[1] + bw[2];
     const uint2* tdata = data + __builtin_amdgcn_readlane((int)offv, k) / 8;
     uint32_t a0 = pa[k].x, a1 = pa[k].y, b0 = 0u, b1 = 0u;   // base bits 0..63, 64..95
-    transpose64(a0, a1, TL);
+    if constexpr (!(SDF_DECODE_SKIP & 1)) transpose64(a0, a1, TL);
     if (B > 64) {   // base planes 64..95: rare (residuals wider than 21 bits on average)
       const uint2 pb = lane + 64 < B ? tdata[64 + lane] : make_uint2(0u, 0u);
       b0 = pb.x;
@@ -188,54 +194,68 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
     // the escapes: masks at qwords B.., then the field-width bytes and the
     // pixel-major fields, a bitstream from qword B + P (P escaped channels):
     // this pixel's fields (all its escaped channels) are one window of <= 36
-    // bits at bit 8 P + sum_c d_c * (outliers of c below this pixel)
+    // bits at bit 8 P + sum_c d_c * (outliers of c below this pixel).  dl[c]:
+    // this pixel's field bits in channel c (d_c for an outlier, else 0, by
+    // one v_cndmask on the mask itself), so the fields are cut out of the
+    // window by v_bfe at the running offset, without 64-bit shifts
     const int P = __builtin_popcount(escaped);
-    uint64_t m[3] = {0ull, 0ull, 0ull}, fields = 0ull;
-    int dlt[3] = {0, 0, 0};
-    if (escaped) {
+    uint32_t dl[3] = {0u, 0u, 0u}, f_lo = 0u, f_hi = 0u;
+    if (!(SDF_DECODE_SKIP & 2) && escaped) {
       const int bs = 2 * (B + P);                       // bitstream's first dword
       const uint32_t deltas = bs < 128 ? (uint32_t)__builtin_amdgcn_readlane(
                                              (int)((bs & 1) ? pa[k].y : pa[k].x), bs >> 1)
                                        : reinterpret_cast<const uint32_t*>(tdata)[bs];
       uint32_t o = 8u * (uint32_t)P;
-      int nb = 0, j = 0;
+      int j = 0;
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) {
         if (!((escaped >> ch) & 1)) continue;
         const int mq = B + j;
+        uint32_t mlo, mhi;
         if (mq < 64) {
-          m[ch] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pa[k].x, mq) |
-                  (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)pa[k].y, mq) << 32;
+          mlo = (uint32_t)__builtin_amdgcn_readlane((int)pa[k].x, mq);
+          mhi = (uint32_t)__builtin_amdgcn_readlane((int)pa[k].y, mq);
         } else {
           const uint2 mm = tdata[mq];
-          m[ch] = (uint64_t)mm.x | (uint64_t)mm.y << 32;
+          mlo = __builtin_amdgcn_readfirstlane(mm.x);
+          mhi = __builtin_amdgcn_readfirstlane(mm.y);
         }
-        dlt[ch] = (int)((deltas >> (8 * j++)) & 255);
-        o += (uint32_t)dlt[ch] * __builtin_amdgcn_mbcnt_hi(
-                                     (uint32_t)(m[ch] >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m[ch], 0u));
-        if ((m[ch] >> lane) & 1) nb += dlt[ch];
+        const uint32_t d = (deltas >> (8 * j++)) & 255u;
+        o += d * __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+        dl[ch] = __builtin_amdgcn_inverse_ballot_w64((uint64_t)mhi << 32 | mlo) ? d : 0u;
       }
+      const uint32_t dw = (uint32_t)bs + (o >> 5);
+#if SDF_DECODE_ESC_VMEM
+      // dwords dw .. dw + 2 of the tile's data, loaded by the lanes with fields
+      uint32_t d0 = 0u, d1 = 0u, d2 = 0u;
+      if (dl[0] | dl[1] | dl[2]) {
+        const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
+        d0 = t32[dw];
+        d1 = t32[dw + 1];
+        d2 = t32[dw + 2];
+      }
+#else
       // dwords dw .. dw + 2 of the tile's data: qwords dw / 2 and dw / 2 + 1
       // from the lanes holding them
-      const uint32_t dw = (uint32_t)bs + (o >> 5);
       const int a = (int)((dw >> 1) << 2);
       const uint32_t s0 = __builtin_amdgcn_ds_bpermute(a, (int)pa[k].x);
       const uint32_t s1 = __builtin_amdgcn_ds_bpermute(a, (int)pa[k].y);
       const uint32_t t0 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].x);
       const uint32_t t1 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].y);
       uint32_t d0 = (dw & 1) ? s1 : s0, d1 = (dw & 1) ? t0 : s1, d2 = (dw & 1) ? t1 : t0;
-      if (nb && dw + 2 >= 128) {   // beyond the loaded qwords: rare
+      if ((dl[0] | dl[1] | dl[2]) && dw + 2 >= 128) {   // beyond the loaded qwords: rare
         const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
         d0 = t32[dw];
         d1 = t32[dw + 1];
         d2 = t32[dw + 2];
       }
-      fields = (uint64_t)__builtin_amdgcn_alignbit(d1, d0, o & 31) |
-               (uint64_t)__builtin_amdgcn_alignbit(d2, d1, o & 31) << 32;
+#endif
+      f_lo = __builtin_amdgcn_alignbit(d1, d0, o & 31);
+      f_hi = __builtin_amdgcn_alignbit(d2, d1, o & 31);
     }
     float v[3];
     int kp = 0;
+    uint32_t sh = 0u;   // this pixel's fields consumed so far (<= 24 bits)
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
       const int w = bw[ch];
@@ -245,13 +265,15 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
                                    : __builtin_amdgcn_alignbit(b1, b0, kp - 64);
       uint32_t z = w ? x & (0xFFFFFFFFu >> (32 - w)) : 0u;
       kp += w;
-      if ((m[ch] >> lane) & 1) {   // this pixel's next field: bits w.. of z
-        z |= ((uint32_t)fields & (0xFFFFFFFFu >> (32 - dlt[ch]))) << w;
-        fields >>= dlt[ch];
+      if ((escaped >> ch) & 1) {   // this pixel's field (dl[ch] bits, 0 if none): bits w.. of z
+        const uint32_t f = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(f_hi, f_lo, sh), 0u, dl[ch]);
+        z |= f << w;
+        sh += dl[ch];
       }
       uint32_t r = (z >> 1) ^ (0u - (z & 1u));            // un-zigzag
       if (lane == 0) r = first[ch];                       // pixel 0 travels raw
-      v[ch] = __uint_as_float(unordered_bits(scan_tile(r, SL)));
+      if constexpr (SDF_DECODE_SKIP & 4) v[ch] = __uint_as_float(r);
+      else v[ch] = __uint_as_float(unordered_bits(scan_tile(r, SL)));
     }
     const int x = tx * 8 + col;
     if (x < width && ty * 8 + prow < rows) {
@@ -264,7 +286,8 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
       }
       const int y = (first_blk + b * period) * brows + w + jb * gap;
       float4 px = make_float4(v[0], v[1], v[2], 1.0f);
-      if (shade == kTilesShadeFast) px = shade_colour<false>(K, v[0], v[1], v[2]);
+      if (SDF_DECODE_SKIP & 8) px = make_float4(v[0], v[1], v[2], 1.0f);
+      else if (shade == kTilesShadeFast) px = shade_colour<false>(K, v[0], v[1], v[2]);
       else if (shade == kTilesShadeExact) px = shade_colour<true>(K, v[0], v[1], v[2]);
       if constexpr (SDF_DECODE_NT) {
         typedef float v4f __attribute__((ext_vector_type(4)));
