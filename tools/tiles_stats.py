@@ -39,6 +39,36 @@ def main():
            "escaped_tile_frac": round(float((esc != 0).mean()), 4),
            "escaped_channel_frac": [round(float(((esc >> c) & 1).mean()), 4) for c in range(3)],
            "qwords_mean": round(float(q.mean()), 2), "qwords_over_64_frac": round(float((q > 64).mean()), 4)}
+    # the residual widths w per tile and channel (tests/tiles_ref.py's
+    # encoder steps on the SHADE32F terms): how often channel pairs fit one
+    # 32-bit word of the encoder's transpose
+    sys.path.insert(0, str(ROOT / "tests"))
+    import tiles_ref as T
+    f.params.output_format = abi.FORMAT_SHADE32F
+    sh, _ = rd.render(f)
+    torch.cuda.synchronize()
+    terms = sh.cpu().numpy()
+    rows, width = terms.shape[:2]
+    n = T.tiles_shape(width, rows)[0] * T.tiles_shape(width, rows)[1]
+    ws = []
+    for c in range(3):
+        u = T.ordered(np.ascontiguousarray(terms[..., c]).view(np.uint32))
+        t = T._tiles(u, rows, width).astype(np.uint64)
+        L = np.zeros_like(t); L[:, :, 1:] = t[:, :, :-1]
+        U = np.zeros_like(t); U[:, 1:, :] = t[:, :-1, :]
+        UL = np.zeros_like(t); UL[:, 1:, 1:] = t[:, :-1, :-1]
+        r = ((t - L - U + UL) & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        r = np.where(r >= 2 ** 31, r - 2 ** 32, r)
+        z = np.where(r >= 0, 2 * r, -2 * r - 1).astype(np.uint64).reshape(n, 64)
+        z[:, 0] = 0
+        ws.append(np.ceil(np.log2(z.max(axis=1).astype(np.float64) + 1)).astype(int))
+    w0, w1, w2 = ws
+    out["w_mean"] = [round(float(w.mean()), 2) for w in ws]
+    out["w_le16"] = [round(float((w <= 16).mean()), 4) for w in ws]
+    out["w0_w2_le16"] = round(float(((w0 <= 16) & (w2 <= 16)).mean()), 4)
+    out["w0_plus_w2_le32"] = round(float((w0 + w2 <= 32).mean()), 4)
+    out["w1_plus_w2_le32"] = round(float((w1 + w2 <= 32).mean()), 4)
+    out["w_sum_le64"] = round(float((w0 + w1 + w2 <= 64).mean()), 4)
     print(json.dumps(out))
 
 
