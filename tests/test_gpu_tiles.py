@@ -267,3 +267,46 @@ def test_frame_rows_tiling_assembles_in_place(renderer, world):
     renderer.tiles_decode(parts, world, stride, w, h, 8, out=out2)
     torch.cuda.synchronize()
     assert same_bits(out2.cpu().numpy(), whole.cpu().numpy())
+
+
+def _tile_widths(terms):
+    """Per tile and channel the widest zigzag residual's bit count (the
+    encoder's w), restated with tests/tiles_ref.py's steps."""
+    rows, width = terms.shape[:2]
+    ty, tx = tiles_ref.tiles_shape(width, rows)
+    ws = []
+    for c in range(3):
+        u = tiles_ref.ordered(np.ascontiguousarray(terms[..., c]).view(np.uint32))
+        t = tiles_ref._tiles(u, rows, width).astype(np.uint64)
+        L = np.zeros_like(t); L[:, :, 1:] = t[:, :, :-1]
+        U = np.zeros_like(t); U[:, 1:, :] = t[:, :-1, :]
+        UL = np.zeros_like(t); UL[:, 1:, 1:] = t[:, :-1, :-1]
+        r = ((t - L - U + UL) & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        r = np.where(r >= 2 ** 31, r - 2 ** 32, r)
+        z = np.where(r >= 0, 2 * r, -2 * r - 1).astype(np.uint64).reshape(ty * tx, 64)
+        z[:, 0] = 0
+        ws.append(tiles_ref._bit_length(z.max(axis=1)))
+    return ws
+
+
+@pytest.mark.parametrize("cfg,w,h,pose", [("C4", 480, 272, 0), ("C5", 320, 200, 0)])
+def test_encoder_narrow_and_wide_tiles(renderer, cfg, w, h, pose):
+    """The encoder's two paths (render_kernel.inc store_tiles, round 4): a
+    tile whose channels 0 and 2 fit 16 bits takes one transpose and one
+    base-width search, any other tile two of each.  Frames holding both
+    kinds encode byte for byte as the NumPy encoder does."""
+    prec = abi.PRECISION_FAST
+    terms = shade_terms(renderer, cfg, w, h, pose, prec)
+    w0, _, w2 = _tile_widths(terms)
+    narrow = (w0 <= 16) & (w2 <= 16)
+    assert 0 < narrow.sum() < narrow.size, "the frame must exercise both encoder paths"
+    _, st = render_pair(renderer, cfg, w, h, pose, prec)
+    s = st.cpu().numpy()
+    s = s[:tiles_ref.stream_bytes(s)]
+    f = frame(cfg, w, h, pose, prec, abi.FORMAT_TILES)
+    e = tiles_ref.encode(terms, tiles_ref.shade_header(f.light, f.material, False))
+    n = narrow.size
+    table_end, head = tiles_ref.HEADER_BYTES + 4 * n, tiles_ref.head_offset(n)
+    assert s.size == e.size
+    assert np.array_equal(s[:table_end], e[:table_end])
+    assert np.array_equal(s[head:], e[head:])
