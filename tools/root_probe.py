@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--shares", default="1:1", help="rank 0 : other ranks, blocks per period")
     ap.add_argument("--streams", type=int, default=3, help="alternating streams / buffers")
     ap.add_argument("--lib", default=None, help="another libsdf3d.so build (A/B)")
+    ap.add_argument("--skip-root-part", action="store_true",
+                    help="decode only the peers' parts (rank 0's empty part not launched)")
     ap.add_argument("--only", choices=["decode", "root", "peer", "peer_plain"], default=None,
                     help="time one leg only (for rocprofv3 counter passes)")
     args = ap.parse_args()
@@ -68,6 +70,11 @@ def main():
     prow = R.owned_rows(H, tilings[busiest])
     peer_plain = [torch.empty((prow, W, 4), dtype=torch.float32, device=rd.device) for _ in range(NS)]
 
+    # the parts the decode is given: all N (rank 0's empty: its header says
+    # ntiles = 0) or, with --skip-root-part, the N - 1 peers' only
+    first = 1 if args.skip_root_part else 0
+    dparts, dN, dtilings = parts[first * stride:], N - first, tilings[first:]
+
     def run(render=True, decode=True, serial=False, peer=False, plain=False):
         pf = f if plain else ft
         for b in range(NS):
@@ -77,7 +84,7 @@ def main():
             if render:
                 rd.render(f, t0_tiling, out=frames[b], stream=streams[b])
             if decode:
-                rd.tiles_decode(parts, N, stride, W, H, 8, tilings=tilings, out=frames[b],
+                rd.tiles_decode(dparts, dN, stride, W, H, 8, tilings=dtilings, out=frames[b],
                                 stream=streams[b] if serial else side)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -91,7 +98,7 @@ def main():
             if render:
                 rd.render(f, t0_tiling, out=frames[b], stream=s)
             if decode:
-                rd.tiles_decode(parts, N, stride, W, H, 8, tilings=tilings, out=frames[b],
+                rd.tiles_decode(dparts, dN, stride, W, H, 8, tilings=dtilings, out=frames[b],
                                 stream=s if serial else side)
         torch.cuda.synchronize()
         return round((time.perf_counter() - t0) / K * 1e3, 4)
