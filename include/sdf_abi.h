@@ -61,7 +61,8 @@ extern "C" {
                                 9: TILES carries shading terms (64-byte
                                    stream header), SDF_FORMAT_SHADE32F;
                                 10: sdf_driver_config.batch (frames per
-                                   ship) */
+                                   ship); TILES base bits pixel by pixel
+                                   (lane-major) instead of bit planes */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -229,9 +230,11 @@ typedef struct {
  *            are 0; mod 2^32; its inverse is the tile's 2-D prefix sum),
  *            zigzag-coded to z, with z := 0 for pixel 0 (it travels raw) and
  *            for pixels outside the frame.  Per channel c the tile stores
- *            b[c] base bit planes (plane k holds bit k of z_j in bit j) and,
- *            when its widest z has w > b[c] bits, an escape: a u64 mask of
- *            the outlier pixels (z_j >= 2^b[c]), a width byte d = w - b[c]
+ *            the low b[c] bits of every z_j, pixel by pixel: b[c] u64 words
+ *            whose bits j b[c] .. j b[c] + b[c] - 1 are z_j's (ABI 10; bit
+ *            planes before), and, when its widest z has w > b[c] bits, an
+ *            escape: a u64 mask of the outlier pixels (z_j >= 2^b[c]), a
+ *            width byte d = w - b[c]
  *            and each outlier's bits b[c].. as a d-bit field.  The encoder
  *            picks b[c] among w, w - 1, .., w - 12 by the smallest size
  *            (64 b + 72 + d * outliers bits; ties: larger b).
@@ -256,8 +259,8 @@ typedef struct {
  *                                   c is escaped (P = popcount(e)),
  *                                   first[c] u of pixel 0
  *              data = head + 16 * ntiles, per tile q u64 words:
- *                                   b0 + b1 + b2 base planes, channel by
- *                                   channel; the P masks of the escaped
+ *                                   b0 + b1 + b2 words of base bits,
+ *                                   channel by channel; the P masks of the escaped
  *                                   channels; then one bitstream (LSB
  *                                   first, zero-padded to whole words):
  *                                   the P width bytes, then the fields

@@ -14,11 +14,11 @@
 //               rows of the assembled frame; a rendered stream's channels
 //               are the pixels' shading terms, made into the colour here
 //               exactly as the render kernel does (shade.h).  Lane j = pixel (j / 8, j % 8):
-//               the planes arrive by one vector load (lane i: plane i), a
-//               64 x 64 bit transpose gives every lane the concatenation of
-//               its three residuals, then un-zigzag and the tile's 2-D
-//               inclusive prefix sum (DPP along rows, ds_bpermute along
-//               columns) invert the gradient predictor in uint32 arithmetic.
+//               each lane loads its own base bits of each channel (stored
+//               pixel by pixel, ABI 10), adds its escaped high bits, then
+//               un-zigzag and the tile's 2-D inclusive prefix sum (DPP along
+//               rows, ds_bpermute along columns) invert the gradient
+//               predictor in uint32 arithmetic.
 //
 // All three move a few bytes per pixel; the decode writes 16 per pixel
 // (RGBA32F); the decode is VALU-issue bound (TILES).
@@ -29,7 +29,6 @@
 #include "kernel_args.h"
 #define SDF_SHADE_LIBRARY_POW 1   // see shade.h spec_pow
 #include "shade.h"
-#include "wave_bits.h"
 
 namespace sdf {
 namespace {
@@ -83,7 +82,7 @@ __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
 #define SDF_DECODE_ESC_VMEM 0   // 1: a pixel's escape window by its own loads, not ds_bpermute
 #endif
 #ifndef SDF_DECODE_SKIP
-#define SDF_DECODE_SKIP 0   // timing probes only (wrong pixels): 1 transpose, 2 escapes, 4 scan, 8 shade
+#define SDF_DECODE_SKIP 0   // timing probes only (wrong pixels): 2 escapes, 4 scan, 8 shade
 #endif
 constexpr int kDecodeTiles = SDF_DECODE_TILES;
 constexpr int kDecodeWgWaves = SDF_DECODE_WG_WAVES;
@@ -91,9 +90,9 @@ constexpr int kDecodeWgWaves = SDF_DECODE_WG_WAVES;
 // One wave = TPW consecutive tiles of one part, lane j = pixel (j / 8, j % 8)
 // of each.  The memory traffic is issued up front in two dependent rounds:
 // the part header with the tiles' offsets and heads (one vector load each,
-// lane i: tile i), then every tile's first 64 planes (lane i: plane i).  Per
-// tile: transpose (lane j gets bit j of every plane: its residuals'
-// concatenation), cut out the three channels, un-zigzag, 2-D prefix sum,
+// lane i: tile i), then every tile's first 64 words (lane i: word i; the
+// escapes' masks and bitstream are read from them).  Per tile: each lane's
+// base bits (its own loads), escaped fields, un-zigzag, 2-D prefix sum,
 // RGBA32F store into the tile's frame rows.
 template <int TPW>
 __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t* __restrict__ parts,
@@ -141,7 +140,6 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
     const uint32_t off = __builtin_amdgcn_readlane((int)offv, k);
     pa[k] = lane < nq ? data[off / 8 + lane] : make_uint2(0u, 0u);
   }
-  const TransposeLanes TL(lane);
   const ScanLanes SL(lane);
   const int col = lane & 7, prow = lane >> 3;
   // tile position, stepped per tile without divisions: tile column tx, tile
@@ -180,13 +178,25 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
     const uint32_t escaped = (head >> 26) & 7;
     const int B = bw[0] + bw[1] + bw[2];
     const uint2* tdata = data + __builtin_amdgcn_readlane((int)offv, k) / 8;
-    uint32_t a0 = pa[k].x, a1 = pa[k].y, b0 = 0u, b1 = 0u;   // base bits 0..63, 64..95
-    if constexpr (!(SDF_DECODE_SKIP & 1)) transpose64(a0, a1, TL);
-    if (B > 64) {   // base planes 64..95: rare (residuals wider than 21 bits on average)
-      const uint2 pb = lane + 64 < B ? tdata[64 + lane] : make_uint2(0u, 0u);
-      b0 = pb.x;
-      b1 = pb.y;
-      transpose64(b0, b1, TL);
+    // this pixel's base bits of each channel (lane-major: bw[c] words per
+    // channel, pixel j's at bit j bw[c]): the two dwords holding them, by the
+    // lane's own loads (no transpose; 0.0383 against 0.0407 ms with the bit
+    // planes' 64 x 64 transpose, profiles/r04_decode_ab.json)
+    uint32_t xb[3];
+    {
+      const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
+      uint32_t kb = 0u;
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) {
+        const uint32_t w = (uint32_t)bw[ch];
+        const uint32_t lbit = 64u * kb + (uint32_t)lane * w;
+        // the second dword only where the bits reach it (never past the
+        // channel's words: a stream may end there)
+        const uint32_t d0 = lbit >> 5, d1 = (lbit & 31u) + w > 32u ? d0 + 1 : d0;
+        xb[ch] = w ? __builtin_amdgcn_alignbit(t32[d1], t32[d0], lbit & 31u) & (0xFFFFFFFFu >> (32u - w))
+                   : 0u;
+        kb += w;
+      }
     }
     const uint32_t first[3] = {(uint32_t)__builtin_amdgcn_readlane((int)hdv.y, k),
                                (uint32_t)__builtin_amdgcn_readlane((int)hdv.z, k),
@@ -254,17 +264,11 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
       f_hi = __builtin_amdgcn_alignbit(d2, d1, o & 31);
     }
     float v[3];
-    int kp = 0;
     uint32_t sh = 0u;   // this pixel's fields consumed so far (<= 24 bits)
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
       const int w = bw[ch];
-      // w bits of the base concatenation from bit kp (kp, w wave-uniform)
-      const uint32_t x = kp < 32   ? __builtin_amdgcn_alignbit(a1, a0, kp)
-                         : kp < 64 ? __builtin_amdgcn_alignbit(b0, a1, kp - 32)
-                                   : __builtin_amdgcn_alignbit(b1, b0, kp - 64);
-      uint32_t z = w ? x & (0xFFFFFFFFu >> (32 - w)) : 0u;
-      kp += w;
+      uint32_t z = xb[ch];
       if ((escaped >> ch) & 1) {   // this pixel's field (dl[ch] bits, 0 if none): bits w.. of z
         const uint32_t f = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(f_hi, f_lo, sh), 0u, dl[ch]);
         z |= f << w;

@@ -65,7 +65,8 @@ def _bit_length(m: np.ndarray) -> np.ndarray:
     return w
 
 
-# Per channel the tile keeps `b` base bit planes of every residual and, when
+# Per channel the tile keeps the low `b` bits of every residual -- b words,
+# pixel j's bits at bit j * b (lane-major, round 4; bit planes before) -- and, when
 # some residuals are wider (the tile's widest has `w` bits), an escape for
 # them: the 64-bit mask M of those pixels, a width byte w - b, and their
 # bits b..w-1 as (w - b)-bit fields.  b is the cheapest of w, w-1, ...,
@@ -145,7 +146,6 @@ def encode(rgb: np.ndarray, shade: tuple[int, np.ndarray] | None = None) -> np.n
         zs.append(z)
         bls.append(bl)
         bases.append(_choose_base(bl))
-    bitpos = np.arange(64, dtype=np.uint64)
     table = np.zeros(n, dtype=np.uint32)
     blocks, off = [], 0
     for i in range(n):
@@ -155,8 +155,13 @@ def encode(rgb: np.ndarray, shade: tuple[int, np.ndarray] | None = None) -> np.n
         for c in range(3):
             z, b = zs[c][i], int(bases[c][i])
             w = int(bls[c][i].max())
-            for p in range(b):
-                base_planes.append(int((((z >> np.uint64(p)) & np.uint64(1)) << bitpos).sum(dtype=np.uint64)))
+            # lane-major: pixel j's low b bits at bit j * b of the channel's
+            # b words
+            low = z & np.uint64((1 << b) - 1) if b else np.zeros(64, dtype=np.uint64)
+            acc = 0
+            for j in range(64 if b else 0):
+                acc |= int(low[j]) << (j * b)
+            base_planes.extend(int(acc >> (64 * p)) & 0xFFFFFFFFFFFFFFFF for p in range(b))
             if b < w:
                 present |= 1 << c
                 o = bls[c][i] > b
@@ -201,7 +206,6 @@ def decode(stream: np.ndarray, width: int, rows: int) -> np.ndarray:
     heads = np.frombuffer(s[head_offset(n):data_offset(n)].tobytes(), dtype=np.uint32).reshape(n, 4)
     base = data_offset(n)
     out = np.ones((ty * 8, tx * 8, 4), dtype=np.float32)
-    bitpos = np.arange(64, dtype=np.uint64)
     for i in range(n):
         h = int(heads[i, 0])
         bs = [h & 63, h >> 6 & 63, h >> 12 & 63]
@@ -218,10 +222,10 @@ def decode(stream: np.ndarray, width: int, rows: int) -> np.ndarray:
         zs = []
         kp = 0
         for c in range(3):
-            z = np.zeros(64, dtype=np.uint64)
-            for p in range(bs[c]):
-                z |= ((q[kp + p] >> bitpos) & np.uint64(1)) << np.uint64(p)
-            kp += bs[c]
+            b = bs[c]
+            acc = int.from_bytes(q[kp:kp + b].tobytes(), "little")
+            z = np.array([acc >> (j * b) & ((1 << b) - 1) for j in range(64)], dtype=np.uint64)
+            kp += b
             zs.append(z)
         pos = 8 * P
         for j in range(64):
