@@ -310,3 +310,25 @@ def test_encoder_narrow_and_wide_tiles(renderer, cfg, w, h, pose):
     assert s.size == e.size
     assert np.array_equal(s[:table_end], e[:table_end])
     assert np.array_equal(s[head:], e[head:])
+
+
+def test_wide_tiles_decode_on_gpu(renderer):
+    """Random 32-bit channel values: tiles whose base bits fill more than 64
+    words (b0 + b1 + b2 up to 96), the words past the decoder's first vector
+    load, read by each lane's own loads (ABI 10's pixel-by-pixel base bits);
+    the stream sits at the very end of its buffer, so no load may run past
+    the tiles' words."""
+    import torch
+    rng = np.random.default_rng(11)
+    w, h = 24, 16
+    a = np.ones((h, w, 4), dtype=np.float32)
+    a[..., :3] = rng.integers(0, 2 ** 32, (h, w, 3), dtype=np.uint32).view(np.float32)
+    s = tiles_ref.encode(a)
+    n = tiles_ref.tiles_shape(w, h)[0] * tiles_ref.tiles_shape(w, h)[1]
+    heads = np.frombuffer(s[tiles_ref.head_offset(n):tiles_ref.data_offset(n)].tobytes(),
+                          dtype=np.uint32).reshape(n, 4)[:, 0]
+    assert ((heads & 63) + (heads >> 6 & 63) + (heads >> 12 & 63) > 64).any()
+    buf = torch.from_numpy(s.copy()).to(renderer.device)   # exactly the stream's bytes
+    out = renderer.tiles_decode(buf, 1, buf.numel(), w, h)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), a)
