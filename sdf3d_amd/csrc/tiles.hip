@@ -1,11 +1,11 @@
 // tiles.hip -- the TILES wire format (sdf_abi.h SDF_FORMAT_TILES) around the
 // render kernel's encoder (render_kernel.inc store_tiles):
 //
-//   compaction  the encoder leaves each tile's planes in a fixed worst-case
-//               slot and its head (plane widths, raw first pixel) in place;
+//   compaction  the encoder leaves each tile's words in a fixed worst-case
+//               slot and its head (base widths, raw first pixel) in place;
 //               tiles_scan turns the widths into block-local offsets and
 //               per-block totals, tiles_move adds the block prefix and copies
-//               each tile's planes into the contiguous stream (kernel_args.h
+//               each tile's words into the contiguous stream (kernel_args.h
 //               TilesLayout).
 //   decode      fused with the multi-device de-interleave: rank r's stream
 //               holds the packed rows of its tiling (the interleave
@@ -311,12 +311,12 @@ __global__ __launch_bounds__(64 * kDecodeWgWaves) void decode_tiles(const Decode
   decode_body<kDecodeTiles>(D, parts, waves_per_part, frame);
 }
 
-// Offsets of the plane blocks in tile order: exclusive scan of 8 * (w0 + w1
+// Offsets of the tiles' word blocks in tile order: exclusive scan of 8 * (w0 + w1
 // + w2) over the heads.  tiles_scan: one wave x 32 consecutive tiles per lane
 // per block of kScanTiles -> block-local offsets + the block's total.
 // tiles_move: one wave per 8 consecutive tiles (in one scan block) adds the
 // block's prefix (the sum of earlier block totals, a wave reduction), writes
-// the final offsets and copies the tiles' planes from their slots into the
+// the final offsets and copies the tiles' words from their slots into the
 // stream, the 8 tiles' loads in flight together (one wave per tile took
 // 30.7 us on a whole 4K frame); the last tile writes `used`.  Both launch
 // one-wave workgroups (round 4): they run beside the next frames' render
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64) void tiles_move(uint8_t* buf, int ntiles, uint3
 #pragma unroll
   for (int s = 32; s >= 1; s >>= 1) pre += (uint32_t)__shfl_xor((int)pre, s);
   uint32_t* table = reinterpret_cast<uint32_t*>(buf + L.table);
-  // lane k < nt: tile t0 + k's block-local offset and plane bytes
+  // lane k < nt: tile t0 + k's block-local offset and data bytes
   const uint32_t loc = lane < nt ? table[t0 + lane] : 0u;
   const uint32_t byt =
       lane < nt ? plane_bytes(reinterpret_cast<const uint4*>(buf + L.head)[t0 + lane].x) : 0u;
