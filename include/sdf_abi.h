@@ -399,6 +399,31 @@ int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
                      int32_t width, int32_t height, int32_t block_rows, void* frame,
                      void* stream);
 
+/* Streams are untrusted input (they crossed a wire): every decode reads only
+ * inside each part's worst-case stream (sdf_tiles_bytes of its rows), and a
+ * malformed part -- header length or tile count that disagrees with the
+ * part, a tile whose offset, size or base widths leave the stream's data, an
+ * escape field beyond its tile -- is skipped (the whole part, or the tiles
+ * concerned: nothing is written for them; every other tile decodes as
+ * usual).  sdf_tiles_decode(_tilings) skip silently;
+ * sdf_tiles_decode_checked reports:
+ *   used    host array of nparts (may be NULL): the data bytes part r must
+ *           hold (its header word 0, e.g. the length the ranks agreed on
+ *           before the transfer), or -1 for "the header's own, within the
+ *           part"; a part expected to carry a stream (used[r] >= 0) whose
+ *           header says none is malformed;
+ *   status  device-writable array of nparts uint32 (may be NULL), zeroed by
+ *           the caller: word r becomes nonzero (SDF_TILES_BAD_* bits) when
+ *           part r is malformed -- asynchronous, like the decode.  With
+ *           status == NULL the call waits for the decode on `stream` and
+ *           returns SDF_E_COMM when some part was malformed. */
+#define SDF_TILES_BAD_HEADER 1u
+#define SDF_TILES_BAD_TILE   2u
+#define SDF_TILES_BAD_FIELD  4u
+int sdf_tiles_decode_checked(const void* parts, int32_t nparts, int64_t part_stride,
+                             const sdf_tiling* tilings, const int64_t* used, int32_t width,
+                             int32_t height, void* frame, uint32_t* status, void* stream);
+
 /* Debug view of the `steps` output of sdf_render: `count` int2 entries
  * (primary, shadow) -> colours of `format`, with which = 0 (primary), 1
  * (shadow) or 2 (their sum), intensity = steps / max_steps mapped through the
@@ -496,9 +521,14 @@ int sdf_driver_step(sdf_driver* driver, int64_t* frame_index);
 /* Ship every rendered frame and wait until all work of this rank is done. */
 int sdf_driver_drain(sdf_driver* driver);
 /* Rank 0 (or world 1): device pointer of frame `index`'s framebuffer
- * (height * width pixels), one of the last nbuf frames.  With collectives
- * the frame must have been shipped (the last `lag` frames stepped are, after
- * sdf_driver_drain): an index not shipped yet is SDF_E_INVALID_ARG. */
+ * (height * width pixels), one of the last nbuf frames whose buffer set no
+ * later frame has taken (after a drain that closed a short batch the next
+ * frames may start on other buffer sets): any other index is
+ * SDF_E_INVALID_ARG.  With collectives the frame must have been shipped (the
+ * last `lag` frames stepped are, after sdf_driver_drain): an index not
+ * shipped yet is SDF_E_INVALID_ARG.  A rank-0 decode that finds a peer's
+ * stream malformed (sdf_tiles_decode_checked) fails the driver: the next
+ * sdf_driver_step or sdf_driver_drain returns SDF_E_COMM. */
 int sdf_driver_frame(sdf_driver* driver, int64_t index, void** rgba);
 /* Copy frame `index` (as sdf_driver_frame) into the caller's device buffer
  * `dst` of `bytes` (>= the frame's size), asynchronously on `stream` after

@@ -49,6 +49,8 @@ FORMAT_NAMES = {"rgba32f": FORMAT_RGBA32F, "rgba16f": FORMAT_RGBA16F, "rgba8": F
 FORMAT_CHANNELS = {FORMAT_RGBA32F: 4, FORMAT_RGBA16F: 4, FORMAT_RGBA8: 4, FORMAT_RGB32F: 3,
                    FORMAT_SHADE32F: 4}
 TILES_HEADER_BYTES = 64   # used, ntiles, shade mode, 0, shading constants (sdf_abi.h)
+# sdf_tiles_decode_checked status bits (sdf_abi.h SDF_TILES_BAD_*)
+TILES_BAD_HEADER, TILES_BAD_TILE, TILES_BAD_FIELD = 1, 2, 4
 
 
 class sdf_primitive(C.Structure):
@@ -131,6 +133,9 @@ SIGNATURES = {
                                    C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_tiles_decode_tilings": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, _P(sdf_tiling),
                                            C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "sdf_tiles_decode_checked": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, _P(sdf_tiling),
+                                           _P(C.c_int64), C.c_int32, C.c_int32, C.c_void_p,
+                                           C.c_void_p, C.c_void_p]),
     "sdf_heatmap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                               C.c_void_p, C.c_void_p]),
     "sdf_render_multi": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light),

@@ -74,6 +74,23 @@ __device__ __forceinline__ float cr_sqrt(float x) {
   return s;
 }
 
+// N square roots behind ONE guard (independent chains stay in one basic
+// block, render_kernel.inc mandelbulb_n): each s[i] == sqrtf(x[i])
+template <int N>
+__device__ __forceinline__ void cr_sqrt_n(const float (&x)[N], float (&s)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    s[i] = sqrt_fast(x[i]);
+    ok = ok & sqrt_fast_ok(x[i]);
+  }
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+#pragma unroll
+    for (int i = 0; i < N; i++) s[i] = sqrt_fast_ok(x[i]) ? s[i] : __builtin_sqrtf(x[i]);
+  }
+}
+
 // 1/x for x in [2^-100, 2^100) (the caller's domain; no guard): v_rcp and
 // one Newton step with an exact fma residual, checked equal to IEEE 1.0f / x
 // on every float of that range
@@ -150,6 +167,31 @@ __device__ __forceinline__ float cr_log(float x) {
     out = ok ? r : (float)log((double)x);
   }
   return out;
+}
+
+// N logs behind ONE guard (as cr_sqrt_n): each out[i] == cr_log(x[i])
+__device__ __forceinline__ bool log_round_ok(float x, double v, float r) {
+  const double tol = SDF_CRM_LOG_EPS * __builtin_fabs(v);
+  return ((float)(v - tol) == r) & ((float)(v + tol) == r) &
+         ((__float_as_uint(x) - 0x00800000u) < (0x7F800000u - 0x00800000u));
+}
+template <int N>
+__device__ __forceinline__ void cr_log_n(const float (&x)[N], float (&out)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const double v = log_fast(x[i]);
+    out[i] = (float)v;
+    ok = ok & log_round_ok(x[i], v, out[i]);
+  }
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const double v = log_fast(x[i]);
+      if (!log_round_ok(x[i], v, out[i])) out[i] = (float)log((double)x[i]);
+    }
+  }
 }
 
 }  // namespace crm

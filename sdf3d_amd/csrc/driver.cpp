@@ -129,6 +129,8 @@ struct sdf_comm {
   Rccl* api;
   ncclComm_t comm;
   int nranks, rank, device;
+  bool nonblocking = false;   // created by ncclCommInitRankConfig, blocking = 0
+  int timeout_ms = 60000;     // the creation's limit, also teardown's
 };
 
 struct sdf_driver {
@@ -156,6 +158,9 @@ struct sdf_driver {
   int32_t* sizes_host = nullptr;
   int32_t* zero_dev = nullptr;
   uint32_t* lens_dev = nullptr;     // per buffer set: its stream's length (tiles_move)
+  // rank 0: per part, nonzero once a decode found that rank's stream
+  // malformed (pinned host memory the decode kernel writes; DecodeParts)
+  uint32_t* bad_host = nullptr;
   std::vector<sdf::RenderPlan> plan_send, plan_frame;
   sdf::DecodeParts decode{};
   std::vector<hipStream_t> rs;      // per buffer set (at most kRenderStreams distinct)
@@ -178,6 +183,11 @@ struct sdf_driver {
   // multiple of `batch`, so that every batch's buffer sets (and lengths) are
   // contiguous
   std::vector<std::pair<long long, int>> frame_buf;
+  // buffer set -> the frame last rendered into it: a frame is handed out only
+  // while its buffer set still holds it (a drain that closes a short batch
+  // moves the next frames onto other buffer sets, so frame_buf alone can name
+  // a set that a later frame has taken over)
+  std::vector<long long> buf_frame;
   long long next = 0;
   long long shipped = -1;  // highest frame whose streams are shipped and decoded (rank 0)
   int error = SDF_OK;  // sticky: a failed driver refuses further frames
@@ -334,6 +344,9 @@ int ship(sdf_driver* d, const sdf_driver::Batch& bt) {
     const int b = bt.b0 + f;
     rc = hip_ok(hipStreamWaitEvent(d->rs[b], d->ev_gather[g], 0));
     if (rc == SDF_OK && d->root) {
+      // each received stream must be exactly the length its rank announced
+      for (int r = 0; r < d->world; ++r)
+        d->decode.used[r] = d->sends[r] ? sz[(size_t)r * d->batch + f] : -1;
       tg = Clock::now();
       rc = hip_ok((hipError_t)sdf::launch_tiles_decode(d->decode, d->frames[b], d->gathered[b],
                                                        d->rs[b]));
@@ -371,6 +384,22 @@ int gather_lengths(sdf_driver* d, long long first, int n, int b0) {
   return SDF_OK;
 }
 
+// A decode found a malformed stream (a truncated or mismatched receive):
+// the ranks no longer agree on what was sent, so the communicators are
+// aborted and the driver fails with SDF_E_COMM.
+int check_streams(sdf_driver* d) {
+  if (!d->bad_host) return SDF_OK;
+  const volatile uint32_t* bad = d->bad_host;
+  for (int r = 0; r < d->world; ++r)
+    if (bad[r] != 0u) {
+      if (debug_on())
+        std::fprintf(stderr, "sdf driver: rank %d's stream was malformed (code %u)\n", r, bad[r]);
+      abort_comms(d);
+      return fail(d, SDF_E_COMM);
+    }
+  return SDF_OK;
+}
+
 void release(sdf_driver* d) {
   (void)hipSetDevice(d->dev);
   for (auto* v : {&d->local, &d->frames, &d->gathered})
@@ -380,6 +409,7 @@ void release(sdf_driver* d) {
   if (d->zero_dev) (void)hipFree(d->zero_dev);
   if (d->lens_dev) (void)hipFree(d->lens_dev);
   if (d->sizes_host) (void)hipHostFree(d->sizes_host);
+  if (d->bad_host) (void)hipHostFree(d->bad_host);
   for (hipStream_t s : d->streams)
     if (s) (void)hipStreamDestroy(s);
   if (d->ss) (void)hipStreamDestroy(d->ss);
@@ -431,13 +461,14 @@ int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32
       if (c) R->CommAbort(c);
       return SDF_E_COMM;
     }
-    sdf_comm probe{R, c, nranks, rank, dev};
-    rc = c ? settle(&probe, ncclInProgress, timeout_ms > 0 ? timeout_ms : 120000) : ncclSystemError;
+    const int limit = timeout_ms > 0 ? timeout_ms : 120000;
+    sdf_comm probe{R, c, nranks, rank, dev, true, limit};
+    rc = c ? settle(&probe, ncclInProgress, limit) : ncclSystemError;
     if (rc != ncclSuccess) {
       if (c) R->CommAbort(c);
       return rc == ncclInProgress ? SDF_E_TIMEOUT : SDF_E_COMM;
     }
-    *comm = new sdf_comm{R, c, nranks, rank, dev};
+    *comm = new sdf_comm{R, c, nranks, rank, dev, true, limit};
     return SDF_OK;
   }
   struct Init {
@@ -471,24 +502,28 @@ int sdf_comm_create(const char* rccl_path, const void* id, int32_t nranks, int32
     return SDF_E_TIMEOUT;
   }
   if (st->rc != ncclSuccess || !st->c) return SDF_E_COMM;
-  *comm = new sdf_comm{R, st->c, nranks, rank, dev};
+  *comm = new sdf_comm{R, st->c, nranks, rank, dev, false,
+                       timeout_ms > 0 ? timeout_ms : 120000};
   return SDF_OK;
 }
 
 // A communicator created non-blocking may answer ncclInProgress while RCCL
-// tears it down.  Where RCCL has ncclCommFinalize, the
-// communicator is finalised first and polled to completion (settle; rccl.h:
-// the state becomes ncclSuccess once it is globally quiescent), then
-// destroyed, which then only frees local resources; a finalise that fails or
-// times out aborts the communicator instead.  Without ncclCommFinalize the
-// destroy is the whole teardown (an ncclInProgress answer is not an error:
-// the handle is gone, so there is nothing left to poll).
+// tears it down.  Where RCCL has ncclCommFinalize, such a
+// communicator is finalised first and polled to completion (settle, within
+// the limit its creation was given; rccl.h: the state becomes ncclSuccess
+// once it is globally quiescent), then destroyed, which then only frees local
+// resources; a finalise that fails or times out aborts the communicator
+// instead.  A blocking communicator (the fallback creation) is not finalised:
+// a blocking ncclCommFinalize could wait without limit for a peer that is
+// gone.  Without ncclCommFinalize the destroy is the whole
+// teardown (an ncclInProgress answer is not an error: the handle is gone, so
+// there is nothing left to poll).
 int sdf_comm_destroy(sdf_comm* comm) {
   if (!comm) return SDF_OK;
   int rc = SDF_OK;
   if (comm->comm) {
-    const int limit = 60000;
-    if (comm->api->CommFinalize) {
+    const int limit = comm->timeout_ms > 0 ? comm->timeout_ms : 60000;
+    if (comm->api->CommFinalize && comm->nonblocking) {
       rc = nccl_ok(settle(comm, comm->api->CommFinalize(comm->comm), limit));
       if (rc != SDF_OK) {
         comm->api->CommAbort(comm->comm);
@@ -544,6 +579,7 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
   d->batch = batch;
   d->ngroups = c.nbuf / batch;
   d->frame_buf.assign(c.nbuf, {-1, 0});
+  d->buf_frame.assign(c.nbuf, -1);
   d->flags = c.flags;
   d->timeout_ms = c.timeout_ms > 0 ? c.timeout_ms : 60000;
   d->collectives = collectives;
@@ -649,6 +685,12 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
     if (rc == SDF_OK)
       rc = hip_ok(hipHostMalloc((void**)&d->sizes_host, sizeof(int32_t) * c.nbuf * c.world,
                                 hipHostMallocDefault));
+    if (d->root && rc == SDF_OK) {
+      rc = hip_ok(hipHostMalloc((void**)&d->bad_host, sizeof(uint32_t) * c.world,
+                                hipHostMallocDefault));
+      if (rc == SDF_OK) std::memset(d->bad_host, 0, sizeof(uint32_t) * c.world);
+      d->decode.status = d->bad_host;
+    }
     d->decode.nparts = c.world;
     d->decode.width = d->W;
     d->decode.height = d->H;
@@ -696,6 +738,7 @@ int sdf_driver_step(sdf_driver* d, int64_t* frame_index) {
 
 static int driver_step(sdf_driver* d, int64_t* frame_index) {
   if (d->error != SDF_OK) return d->error;
+  if (check_streams(d) != SDF_OK) return d->error;
   if (hipSetDevice(d->dev) != hipSuccess) return fail(d, SDF_E_HIP);
   const long long i = d->next;
   const int b = d->buf_next;
@@ -712,6 +755,7 @@ static int driver_step(sdf_driver* d, int64_t* frame_index) {
   if (frame_index) *frame_index = i;
   d->next = i + 1;
   d->frame_buf[i % d->nbuf] = {i, b};
+  d->buf_frame[b] = i;
   d->buf_next = (b + 1) % d->nbuf;
   if (!d->collectives) return SDF_OK;
   rc = hip_ok(hipEventRecord(d->ev_render[b], s));
@@ -772,7 +816,7 @@ static int driver_drain(sdf_driver* d) {
     const int rc = host_wait(d, [s] { return hipStreamQuery(s); });
     if (rc != SDF_OK) return rc;
   }
-  return SDF_OK;
+  return check_streams(d);   // every decode has completed
 }
 
 int sdf_driver_frame(sdf_driver* d, int64_t index, void** rgba) {
@@ -784,7 +828,7 @@ int sdf_driver_frame(sdf_driver* d, int64_t index, void** rgba) {
   // shipped (the last `lag` frames stepped: after sdf_driver_drain)
   if (d->collectives && index > d->shipped) return SDF_E_INVALID_ARG;
   const auto& fb = d->frame_buf[index % d->nbuf];
-  if (fb.first != index) return SDF_E_INVALID_ARG;
+  if (fb.first != index || d->buf_frame[fb.second] != index) return SDF_E_INVALID_ARG;
   *rgba = d->frames[fb.second];
   return SDF_OK;
 }

@@ -150,7 +150,25 @@ struct DecodeParts {
   // part r's stream at part_ptr[r] when non-null (another device's memory,
   // peer-mapped: sdf_render_multi), else at parts + r * part_stride
   const void* part_ptr[SDF_MAX_DECODE_PARTS];
+  // A stream is untrusted input (it crossed RCCL): the decoder reads nothing
+  // outside the part's worst-case stream.  used[r] >= 0: the data bytes part
+  // r must hold (the length the ranks agreed on; its header word 0 must say
+  // the same); -1: the header's word 0, at most the part's capacity.
+  long long used[SDF_MAX_DECODE_PARTS];
+  // device-writable, nparts words (may be null): word r is set to a nonzero
+  // kTilesBad* code when part r is malformed (the decoder then skips the
+  // part, or the tiles that are out of bounds, and writes nothing for them)
+  uint32_t* status;
+  // everything zero, no expected lengths (used = -1), no status words
+  __host__ DecodeParts() {
+    __builtin_memset(this, 0, sizeof(*this));
+    for (int r = 0; r < SDF_MAX_DECODE_PARTS; ++r) used[r] = -1;
+  }
 };
+// (sdf_abi.h SDF_TILES_BAD_*)
+constexpr uint32_t kTilesBadHeader = SDF_TILES_BAD_HEADER;   // length / tile count disagree
+constexpr uint32_t kTilesBadTile = SDF_TILES_BAD_TILE;       // a tile's offset, size or widths
+constexpr uint32_t kTilesBadField = SDF_TILES_BAD_FIELD;     // an escape field past its tile
 int launch_tiles_decode(const DecodeParts& d, void* frame, const void* parts, void* stream);
 
 // ---- TILES stream buffer (sdf_abi.h SDF_FORMAT_TILES) ----------------------

@@ -553,6 +553,15 @@ int sdf_owned_rows(int32_t height, const sdf_tiling* tiling) {
   return count_rows(height, tiling ? *tiling : kWholeFrame);
 }
 
+// Working range of the kernels: every coordinate, size and distance at most
+// 1e15 in magnitude (and capsules of positive length), so that no square,
+// dot product or distance the scene evaluation forms overflows -- every
+// primitive value is then finite and the accumulated scene distance is never
+// NaN, which the exact kernel's hardware minimum relies on (render_kernel.inc
+// smin<HW>).
+constexpr float kMaxCoord = 1e15f;
+constexpr float kMinCapsule2 = 1e-30f;
+
 int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
                  const sdf_material* material, const sdf_params* params,
                  const sdf_tiling* tiling) {
@@ -588,7 +597,13 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
                           pr.op == SDF_OP_SMOOTH_INTERSECT;
       if (smooth && !(pr.k > 0.0f && std::isfinite(pr.k))) return SDF_E_INVALID_ARG;
       for (float v : pr.p)
-        if (!std::isfinite(v)) return SDF_E_INVALID_ARG;
+        if (!std::isfinite(v) || std::fabs(v) > kMaxCoord) return SDF_E_INVALID_ARG;
+      if (smooth && pr.k > kMaxCoord) return SDF_E_INVALID_ARG;
+      if (pr.kind == SDF_PRIM_CAPSULE) {
+        // a segment, not a point: h = dot(pa, ba) / dot(ba, ba) must be a number
+        const float bax = pr.p[3] - pr.p[0], bay = pr.p[4] - pr.p[1], baz = pr.p[5] - pr.p[2];
+        if (!(bax * bax + bay * bay + baz * baz >= kMinCapsule2)) return SDF_E_INVALID_ARG;
+      }
     }
   } else if (scene->kind == SDF_SCENE_MANDELBULB) {
     if (!(scene->bulb_scale > 0.0f) || !finite3(scene->bulb_center)) return SDF_E_INVALID_ARG;
@@ -608,6 +623,12 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   if (!finite3(light->pos)) return SDF_E_INVALID_ARG;
   float inv[16];
   if (!invert_view(camera->view, inv)) return SDF_E_INVALID_ARG;
+  for (float v : inv)
+    if (!(std::fabs(v) <= kMaxCoord)) return SDF_E_INVALID_ARG;
+  for (int i = 0; i < 3; ++i)
+    if (std::fabs(camera->eye[i]) > kMaxCoord || std::fabs(light->pos[i]) > kMaxCoord)
+      return SDF_E_INVALID_ARG;
+  if (std::fabs(p.max_dist) > kMaxCoord) return SDF_E_INVALID_ARG;
   (void)material;
   return SDF_OK;
 }
@@ -673,13 +694,17 @@ int sdf_scene_bounds(const sdf_scene* scene, float* bounds, float* cluster,
   return SDF_OK;
 }
 
-int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_stride,
-                             const sdf_tiling* tilings, int32_t width, int32_t height,
-                             void* frame, void* stream) {
+namespace {
+int decode_parts(const void* parts, int32_t nparts, int64_t part_stride, const sdf_tiling* tilings,
+                 const int64_t* used, int32_t width, int32_t height, void* frame, uint32_t* status,
+                 void* stream) {
   if (!parts || !frame || !tilings || nparts <= 0 || nparts > SDF_MAX_DECODE_PARTS ||
       width <= 0 || height <= 0)
     return SDF_E_INVALID_ARG;
   sdf::DecodeParts d{};
+  d.status = status;
+  if (used)
+    for (int r = 0; r < nparts; ++r) d.used[r] = used[r] < 0 ? -1 : used[r];
   d.nparts = nparts;
   d.width = width;
   d.height = height;
@@ -700,6 +725,36 @@ int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_str
   }
   const int err = sdf::launch_tiles_decode(d, frame, parts, stream);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
+}
+}  // namespace
+
+int sdf_tiles_decode_tilings(const void* parts, int32_t nparts, int64_t part_stride,
+                             const sdf_tiling* tilings, int32_t width, int32_t height,
+                             void* frame, void* stream) {
+  return decode_parts(parts, nparts, part_stride, tilings, nullptr, width, height, frame, nullptr,
+                      stream);
+}
+
+int sdf_tiles_decode_checked(const void* parts, int32_t nparts, int64_t part_stride,
+                             const sdf_tiling* tilings, const int64_t* used, int32_t width,
+                             int32_t height, void* frame, uint32_t* status, void* stream) {
+  if (status)
+    return decode_parts(parts, nparts, part_stride, tilings, used, width, height, frame, status,
+                        stream);
+  // synchronous: status words of the library's own (pinned host memory the
+  // device writes), read once the decode is done
+  if (nparts <= 0 || nparts > SDF_MAX_DECODE_PARTS) return SDF_E_INVALID_ARG;
+  uint32_t* st = nullptr;
+  if (hipHostMalloc((void**)&st, sizeof(uint32_t) * nparts, hipHostMallocDefault) != hipSuccess)
+    return SDF_E_HIP;
+  std::memset(st, 0, sizeof(uint32_t) * nparts);
+  int rc = decode_parts(parts, nparts, part_stride, tilings, used, width, height, frame, st, stream);
+  if (rc == SDF_OK && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = SDF_E_HIP;
+  if (rc == SDF_OK)
+    for (int r = 0; r < nparts; ++r)
+      if (st[r]) rc = SDF_E_COMM;
+  (void)hipHostFree(st);
+  return rc;
 }
 
 int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride, int32_t width,

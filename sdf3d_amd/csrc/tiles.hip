@@ -84,6 +84,15 @@ __device__ __forceinline__ uint32_t unordered_bits(uint32_t u) {
 #ifndef SDF_DECODE_SKIP
 #define SDF_DECODE_SKIP 0   // timing probes only (wrong pixels): 2 escapes, 4 scan, 8 shade
 #endif
+// The macros above are experiment knobs (tools/flag_variant.py, which
+// defines SDF_EXPERIMENT); SKIP builds decode wrong pixels on purpose, and
+// none of them enters sdf_kernel_id, so a library built with any of them
+// away from its default must not pass for a product build.
+#if !defined(SDF_EXPERIMENT) && (SDF_DECODE_SKIP != 0 || SDF_DECODE_ESC_VMEM != 0 || \
+                                 SDF_DECODE_TILES != 4 || SDF_DECODE_WG_WAVES != 4 || \
+                                 SDF_DECODE_NT != 1)
+#error "decoder probe / layout knobs build only as experiments (tools/flag_variant.py)"
+#endif
 constexpr int kDecodeTiles = SDF_DECODE_TILES;
 constexpr int kDecodeWgWaves = SDF_DECODE_WG_WAVES;
 
@@ -113,13 +122,29 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
                                          : parts + (long long)part * D.part_stride;
   const TilesLayout Lt(ntiles);
   const int nt = min(TPW, ntiles - tbase);
-  // the header word is loaded with the tables (a part with ntiles = 0 holds
+  // the header words are loaded with the tables (a part with ntiles = 0 holds
   // no tables, but they lie inside its pitch and are discarded)
+  const uint32_t hused = reinterpret_cast<const uint32_t*>(base)[0];
   const uint32_t present = reinterpret_cast<const uint32_t*>(base)[1];
   const uint32_t offv = lane < nt ? reinterpret_cast<const uint32_t*>(base + Lt.table)[tbase + lane] : 0u;
   const uint4 hdv = lane < nt ? reinterpret_cast<const uint4*>(base + Lt.head)[tbase + lane]
                               : make_uint4(0u, 0u, 0u, 0u);
-  if (present == 0) return;   // no stream: rows rendered in place
+  const long long want = D.used[part];
+  // a malformed part is reported (lane 0's store: a vector store) and skipped
+  auto report = [&](uint32_t code) {
+    if (D.status && lane == 0) D.status[part] = code;
+  };
+  if (present == 0) {   // no stream: rows rendered in place -- unless one was sent
+    if (want >= 0) report(kTilesBadHeader);
+    return;
+  }
+  // the stream's data bytes: what the ranks agreed on, within the part's
+  // worst case (ntiles comes from the host's tiling, not from the stream)
+  const uint32_t cap = (uint32_t)ntiles * (uint32_t)kTilePlaneBytes;
+  if (present != (uint32_t)ntiles || hused > cap || (want >= 0 && (long long)hused != want)) {
+    report(kTilesBadHeader);
+    return;
+  }
   // what the channels hold, and the frame's shading constants (header words
   // 2, 4..13: scalar loads)
   const uint32_t* const hw = reinterpret_cast<const uint32_t*>(base);
@@ -134,12 +159,26 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
   K.shin = __uint_as_float(hw[13]);
   const uint2* data = reinterpret_cast<const uint2*>(base + Lt.data);
   uint2 pa[TPW];   // lane i: qword i of each tile's data (up to 64)
+  // tile k's words lie in the stream's data, [off, off + 8 nq) within
+  // [0, hused), and hold its base words and escape masks (B + P qwords) and,
+  // when it escapes, the bitstream's first qword; each base width is at most
+  // 32 (scalar checks; bit k of `good`).  Every later read of the tile
+  // stays inside its nq qwords (the escape window is checked per lane).
+  uint32_t good = 0u;
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
-    const int nq = k < nt ? (int)tile_qwords(__builtin_amdgcn_readlane((int)hdv.x, k)) : 0;
+    const uint32_t head = (uint32_t)__builtin_amdgcn_readlane((int)hdv.x, k);
     const uint32_t off = __builtin_amdgcn_readlane((int)offv, k);
+    const uint32_t nqk = tile_qwords(head);
+    const uint32_t b0 = head & 63u, b1 = (head >> 6) & 63u, b2 = (head >> 12) & 63u;
+    const uint32_t P = (uint32_t)__builtin_popcount((head >> 26) & 7u);
+    const bool ok = k < nt && (off & 7u) == 0u && off <= hused && 8u * nqk <= hused - off &&
+                    max(b0, max(b1, b2)) <= 32u && b0 + b1 + b2 + P + (P ? 1u : 0u) <= nqk;
+    good |= (uint32_t)ok << k;
+    const int nq = ok ? (int)nqk : 0;
     pa[k] = lane < nq ? data[off / 8 + lane] : make_uint2(0u, 0u);
   }
+  if (good != (nt >= 32 ? ~0u : (1u << nt) - 1u)) report(kTilesBadTile);
   const ScanLanes SL(lane);
   const int col = lane & 7, prow = lane >> 3;
   // tile position, stepped per tile without divisions: tile column tx, tile
@@ -156,6 +195,7 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
     if (k >= nt) continue;
+    // (a malformed tile is skipped below, after the position step)
     if (k > 0 && ++tx == tiles_x) {
       tx = 0;
       ++ty;
@@ -172,6 +212,7 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
         wb = within;
       }
     }
+    if (!((good >> k) & 1u)) continue;
     const uint32_t head = __builtin_amdgcn_readlane((int)hdv.x, k);
     const int bw[3] = {(int)(head & 63), (int)((head >> 6) & 63), (int)((head >> 12) & 63)};
     const int nq = (int)tile_qwords(head);
@@ -235,10 +276,14 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
         dl[ch] = __builtin_amdgcn_inverse_ballot_w64((uint64_t)mhi << 32 | mlo) ? d : 0u;
       }
       const uint32_t dw = (uint32_t)bs + (o >> 5);
+      // the window must lie in the tile's words (malformed masks or widths
+      // could point past them): such a lane loads nothing, the part is reported
+      const bool inside = dw + 2u < 2u * (uint32_t)nq;
+      if (__builtin_amdgcn_ballot_w64((dl[0] | dl[1] | dl[2]) && !inside)) report(kTilesBadField);
 #if SDF_DECODE_ESC_VMEM
       // dwords dw .. dw + 2 of the tile's data, loaded by the lanes with fields
       uint32_t d0 = 0u, d1 = 0u, d2 = 0u;
-      if (dl[0] | dl[1] | dl[2]) {
+      if ((dl[0] | dl[1] | dl[2]) && inside) {
         const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
         d0 = t32[dw];
         d1 = t32[dw + 1];
@@ -253,7 +298,7 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
       const uint32_t t0 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].x);
       const uint32_t t1 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].y);
       uint32_t d0 = (dw & 1) ? s1 : s0, d1 = (dw & 1) ? t0 : s1, d2 = (dw & 1) ? t1 : t0;
-      if ((dl[0] | dl[1] | dl[2]) && dw + 2 >= 128) {   // beyond the loaded qwords: rare
+      if ((dl[0] | dl[1] | dl[2]) && dw + 2 >= 128 && inside) {   // beyond the loaded qwords: rare
         const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
         d0 = t32[dw];
         d1 = t32[dw + 1];

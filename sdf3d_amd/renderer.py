@@ -287,3 +287,33 @@ class Renderer:
                                                        self._stream(stream))
         abi.check(rc, "sdf_tiles_decode")
         return out
+
+    def tiles_decode_checked(self, parts, nparts: int, part_stride: int, width: int, height: int,
+                             tilings, used=None, out=None, status=None, stream=None):
+        """sdf_tiles_decode_checked: the decode of tiles_decode(tilings=...)
+        for streams that crossed a wire.  `used`: each part's expected data
+        bytes (-1: its header's); `status`: a uint32 device tensor of nparts
+        words (zeroed here) that receives each part's SDF_TILES_BAD_* bits,
+        or None for a synchronous call that raises (SDF_E_COMM) when some
+        part was malformed.  Returns (frame, status)."""
+        torch = self.torch
+        if out is None:
+            out = torch.empty((height, width, 4), dtype=torch.float32, device=self.device)
+        if parts.dtype != torch.uint8 or not parts.is_contiguous() \
+                or parts.numel() < nparts * part_stride or out.dtype != torch.float32 \
+                or tuple(out.shape) != (height, width, 4) or not out.is_contiguous() \
+                or len(tilings) != nparts:
+            raise ValueError("TILES parts / RGBA32F frame of the wrong size, layout or type")
+        if status is not None:
+            if status.dtype != torch.int32 or status.numel() < nparts or not status.is_contiguous():
+                raise ValueError("status: nparts int32 words (holding uint32 codes)")
+            status.zero_()
+        arr = (abi.sdf_tiling * nparts)(*tilings)
+        u = None if used is None else (C.c_int64 * nparts)(*[int(x) for x in used])
+        with self._on_device():
+            rc = self.lib.sdf_tiles_decode_checked(
+                C.c_void_p(parts.data_ptr()), nparts, part_stride, arr, u, width, height,
+                C.c_void_p(out.data_ptr()),
+                None if status is None else C.c_void_p(status.data_ptr()), self._stream(stream))
+        abi.check(rc, "sdf_tiles_decode_checked")
+        return out, status

@@ -117,7 +117,21 @@ struct Op {  // one send or receive of a group, progressed chunk by chunk
   size_t bytes;
   int peer;
   size_t chunk = 0, nchunks = 0;
+  int ordinal = 0;   // receives: 1, 2, ... in issue order (fault injection)
 };
+
+// Fault injection (tests only): SHMCOMM_CORRUPT_RECV=k overwrites bytes
+// 64..127 of the k-th receive of this process with 0xFF once its first chunk
+// has landed -- a TILES stream's offset table, i.e. a receive whose content
+// no longer matches its header (tests/test_gpu_driver.py).
+int corrupt_recv_ordinal() {
+  static const int k = [] {
+    const char* e = std::getenv("SHMCOMM_CORRUPT_RECV");
+    return e ? std::atoi(e) : 0;
+  }();
+  return k;
+}
+std::atomic<int> g_recv_ops{0};
 
 }  // namespace
 
@@ -237,6 +251,17 @@ bool progress(ncclComm* c, Op& op) {
       if (ch->sent.load(std::memory_order_acquire) < k + 1) break;
       if (!copy(c, op.dev + off, c->ch_buf(op.peer, c->rank, k), n, hipMemcpyHostToDevice))
         return false;
+      if (op.chunk == 0 && n >= 128 && op.ordinal == corrupt_recv_ordinal()) {
+        static const unsigned char ff[64] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                             0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF};
+        if (!copy(c, op.dev + 64, ff, sizeof(ff), hipMemcpyHostToDevice)) return false;
+      }
       c->taken[op.peer] = k + 1;
       ch->taken.store(k + 1, std::memory_order_release);
     }
@@ -719,6 +744,7 @@ ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatyp
 ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer,
                       ncclComm_t c, hipStream_t stream) {
   Op op{false, static_cast<char*>(recvbuff), count * dtype_size(datatype), peer};
+  op.ordinal = ++g_recv_ops;
   return enqueue(c, op, stream);
 }
 

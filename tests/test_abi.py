@@ -93,6 +93,12 @@ def test_validate_accepts_all_configs():
     lambda f: setattr(f.scene, "kind", 5),
     lambda f: [f.camera.view.__setitem__(i, 0.0) for i in range(16)],  # singular V_mat
     lambda f: f.camera.eye.__setitem__(0, float("inf")),
+    # working range (no overflow, so the scene distance is never NaN)
+    lambda f: f.scene.prims[1].p.__setitem__(3, 2e15),
+    lambda f: f.camera.eye.__setitem__(1, -3e15),
+    lambda f: f.light.pos.__setitem__(2, 1e16),
+    lambda f: setattr(f.params, "max_dist", 1e16),
+    lambda f: [f.camera.view.__setitem__(i, 1e-16 if i % 5 == 0 else 0.0) for i in range(15)],
 ])
 def test_validate_rejects(mutate):
     f = scenes.reference()
@@ -251,3 +257,16 @@ def test_validate_mandelbulb_bailout(bailout, ok):
     f = scenes.config("C5", 64, 36)
     f.scene.bulb_bailout = bailout
     assert _validate(f) == (abi.SDF_OK if ok else abi.SDF_E_INVALID_ARG)
+
+
+def test_validate_rejects_degenerate_capsule():
+    """A capsule whose end points coincide has h = dot(pa, ba) / dot(ba, ba)
+    = 0 / 0: refused (every primitive value must be a number)."""
+    f = scenes.config("C3", 64, 64)
+    cap = [i for i in range(f.scene.count) if f.scene.prims[i].kind == abi.PRIM_CAPSULE]
+    assert cap
+    pr = f.scene.prims[cap[0]]
+    assert _validate(f) == abi.SDF_OK
+    for j in range(3):
+        pr.p[3 + j] = pr.p[j]
+    assert _validate(f) == abi.SDF_E_INVALID_ARG

@@ -243,3 +243,24 @@ def test_cpp_driver_multirank_arcball(tmp_path, world):
     assert np.abs(img.astype(int) - want.astype(int)).max() <= 1
     ref, rst = oracle.render(f)
     assert_parity(compare(f, rgba, st, ref, rst), what="arcball")
+
+
+def test_native_driver_refuses_malformed_stream():
+    """a receive whose content no longer matches its header
+    (the stand-in overwrites frame 2's offset table) makes rank 0's decode
+    skip the bad tiles and the driver fail with SDF_E_COMM -- no fault, the
+    frame before it and frame 2's other tiles intact."""
+    import json
+    import subprocess
+    import sys
+    from netutil import free_port
+    from sdf3d_amd import abi
+    env = dict(os.environ, SHMCOMM_CORRUPT_RECV="3", SHMCOMM_TIMEOUT_MS="20000",
+               GPU_MAX_HW_QUEUES="8")
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "driver_fault_probe.py"),
+                        str(free_port())], capture_output=True, text=True, timeout=180,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["error"] == abi.SDF_E_COMM, d
+    assert d["frame1_exact"] and d["frame2_exact_outside"], d

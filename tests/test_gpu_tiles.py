@@ -332,3 +332,135 @@ def test_wide_tiles_decode_on_gpu(renderer):
     out = renderer.tiles_decode(buf, 1, buf.numel(), w, h)
     torch.cuda.synchronize()
     assert same_bits(out.cpu().numpy(), a)
+
+
+# ---- malformed streams: the decoder must refuse, not fault --
+
+def _stream_fields(st, n):
+    """(table offsets, head word 0s, data offset, used) of a stream on the host."""
+    s = st.cpu().numpy()
+    used = int(s[:4].view(np.uint32)[0])
+    table = s[tiles_ref.HEADER_BYTES:tiles_ref.HEADER_BYTES + 4 * n].view(np.uint32).copy()
+    heads = s[tiles_ref.head_offset(n):tiles_ref.data_offset(n)].view(np.uint32).reshape(n, 4)
+    return table, heads[:, 0].copy(), tiles_ref.data_offset(n), used
+
+
+def _tile_mask(w, h, tiles):
+    """Pixels (h, w) of the given tile indices (row-major 8x8 tiles, row 0 bottom)."""
+    tx = (w + 7) // 8
+    m = np.zeros((h, w), dtype=bool)
+    for t in tiles:
+        y, x = divmod(int(t), tx)
+        m[8 * y:8 * y + 8, 8 * x:8 * x + 8] = True
+    return m
+
+
+def test_malformed_streams_are_refused(renderer):
+    """A truncated or mismatched receive, a corrupted offset table, an
+    impossible tile head and an escape field past its tile: the decode reads
+    nothing outside the part, reports the part (SDF_TILES_BAD_* in its status
+    word; SDF_E_COMM from the synchronous call), writes nothing for the bad
+    tiles and decodes every other tile bit for bit."""
+    import torch
+    w, h = 160, 96
+    ref, st = render_pair(renderer, "C3", w, h, 1, abi.PRECISION_EXACT)
+    refn = ref.cpu().numpy()
+    n = ((w + 7) // 8) * ((h + 7) // 8)
+    table, heads, data0, used = _stream_fields(st, n)
+    whole = [R.tiling(0, 1, h)]
+    status = torch.zeros(1, dtype=torch.int32, device=renderer.device)
+
+    def decode(buf, used_=None):
+        out = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device=renderer.device)
+        renderer.tiles_decode_checked(buf, 1, buf.numel(), w, h, whole, used=used_, out=out,
+                                      status=status)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), int(status.cpu().numpy()[0]) & 0xFFFFFFFF
+
+    # intact, with and without the agreed length: decodes, status 0
+    out, code = decode(st, [used])
+    assert code == 0 and same_bits(out, refn)
+    # the receive got a different length than the header's: whole part skipped
+    for bad_len in (used - 8, used + 8, 0):
+        out, code = decode(st, [bad_len])
+        assert code == abi.TILES_BAD_HEADER and np.isnan(out).all()
+    with pytest.raises(RuntimeError, match="-5|COMM|collective"):
+        renderer.tiles_decode_checked(st, 1, st.numel(), w, h, whole, used=[used - 8])
+    # header claims more data than the part can hold
+    b = st.clone()
+    b[0:4] = torch.tensor([0xFF, 0xFF, 0xFF, 0x7F], dtype=torch.uint8)
+    out, code = decode(b)
+    assert code == abi.TILES_BAD_HEADER and np.isnan(out).all()
+    # truncated: the stream's second half never arrived (zeros), its header
+    # says so -- the tiles whose words lie past it are skipped
+    half = (used // 2) & ~7
+    b = st.clone()
+    b[data0 + half:] = 0
+    b[0:4] = torch.from_numpy(np.array([half], dtype=np.uint32).view(np.uint8)).to(b.device)
+    nq = (heads >> 18) & 255
+    cut = np.nonzero(table.astype(np.int64) + 8 * nq > half)[0]
+    assert 0 < cut.size < n
+    out, code = decode(b)
+    m = _tile_mask(w, h, cut)
+    assert code == abi.TILES_BAD_TILE
+    assert np.isnan(out[m]).all() and same_bits(out[~m], refn[~m])
+    # corrupted table entries and an impossible base width
+    b = st.clone()
+    bad = {3: 0xFFFFFF00, 17: used + 64, 40: 4}   # far away, past the data, misaligned
+    t2 = table.copy()
+    for t, v in bad.items():
+        t2[t] = v
+    b[tiles_ref.HEADER_BYTES:tiles_ref.HEADER_BYTES + 4 * n] = torch.from_numpy(
+        t2.view(np.uint8)).to(b.device)
+    h2 = heads.copy()
+    h2[55] = (h2[55] & ~np.uint32(63)) | np.uint32(40)   # channel 0 base width 40 > 32
+    hb = st[tiles_ref.head_offset(n):data0].cpu().numpy().view(np.uint32).reshape(n, 4).copy()
+    hb[:, 0] = h2
+    b[tiles_ref.head_offset(n):data0] = torch.from_numpy(hb.reshape(-1).view(np.uint8)).to(b.device)
+    out, code = decode(b)
+    m = _tile_mask(w, h, [*bad, 55])
+    assert code == abi.TILES_BAD_TILE
+    assert np.isnan(out[m]).all() and same_bits(out[~m], refn[~m])
+    # an escape field pointing past its tile: a tile with escapes gets width
+    # byte 255 (its fields' offsets then leave the tile's words)
+    esc = np.nonzero((heads >> 26) & 7)[0]
+    assert esc.size > 0
+    t = int(esc[0])
+    B = int((heads[t] & 63) + (heads[t] >> 6 & 63) + (heads[t] >> 12 & 63))
+    P = int(bin(int(heads[t] >> 26) & 7).count("1"))
+    at = data0 + int(table[t]) + 8 * (B + P)   # first byte of the bitstream: channel widths
+    b = st.clone()
+    b[at:at + P] = 255
+    out, code = decode(b)
+    assert code & abi.TILES_BAD_FIELD
+    m = _tile_mask(w, h, [t])
+    assert same_bits(out[~m], refn[~m])
+
+
+def test_malformed_part_among_good_ones(renderer):
+    """Several parts in one decode: only the malformed part is reported and
+    left out; the other parts' rows come out bit-exact."""
+    import torch
+    world, w, h = 3, 96, 80
+    f = frame("C3", w, h, 2, abi.PRECISION_FAST, abi.FORMAT_RGBA32F)
+    whole, _ = renderer.render(f)
+    tilings = [R.tiling(r, world, 8) for r in range(world)]
+    stride = max(R.tiles_bytes(w, R.owned_rows(h, t)) for t in tilings)
+    parts = torch.zeros(world * stride, dtype=torch.uint8, device=renderer.device)
+    ft = frame("C3", w, h, 2, abi.PRECISION_FAST, abi.FORMAT_TILES)
+    for r in range(world):
+        renderer.render(ft, tilings[r], out=parts[r * stride:(r + 1) * stride])
+    torch.cuda.synchronize()
+    used = [int(parts[r * stride:r * stride + 4].cpu().numpy().view(np.uint32)[0])
+            for r in range(world)]
+    status = torch.zeros(world, dtype=torch.int32, device=renderer.device)
+    out = torch.full((h, w, 4), float("nan"), dtype=torch.float32, device=renderer.device)
+    renderer.tiles_decode_checked(parts, world, stride, w, h, tilings,
+                                  used=[used[0], used[1] + 16, used[2]], out=out, status=status)
+    torch.cuda.synchronize()
+    assert status.cpu().numpy().tolist() == [0, abi.TILES_BAD_HEADER, 0]
+    o, wn = out.cpu().numpy(), whole.cpu().numpy()
+    rows1 = np.zeros(h, dtype=bool)
+    for y in range(h):
+        rows1[y] = (y // 8) % world == 1
+    assert np.isnan(o[rows1]).all() and same_bits(o[~rows1], wn[~rows1])

@@ -23,10 +23,11 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     name, flags = sys.argv[1], sys.argv[2:]
+    flags = ["-DSDF_EXPERIMENT=1", *flags]   # unlocks the experiment-only knobs (tiles.hip)
     prefixes = ("render_",)
-    if flags and flags[0].startswith("--units="):
-        prefixes = tuple(flags[0].split("=", 1)[1].split(","))
-        flags = flags[1:]
+    if len(flags) > 1 and flags[1].startswith("--units="):
+        prefixes = tuple(flags[1].split("=", 1)[1].split(","))
+        flags = [flags[0], *flags[2:]]
     from sdf3d_amd import build as b
     b.build_library(verbose=False)
     out = ROOT / "tools" / "_variants" / name
