@@ -370,6 +370,31 @@ int sdf_render(const sdf_scene* scene, const sdf_camera* camera,
                const sdf_params* params, const sdf_tiling* tiling,
                void* rgba, int32_t* steps, void* stream);
 
+/* Render schedules.  A frame's cost is uneven: grazing rays near the horizon
+ * march long, so a launch whose last waves hold the costliest tiles ends
+ * with most of the GPU idle.  sdf_render_scheduled is sdf_render dispatching
+ * the rows' 8-row blocks in the order a schedule keeps: the kernel adds
+ * every wave's shader-clock cycles to its block's counter, the schedule
+ * reads the counters back every `period` launches without waiting (pinned
+ * copy behind the launch, event polled at the next call), and later launches
+ * take the blocks costliest first.  Any order renders every block exactly
+ * once: the output is bit-identical to sdf_render's.  A schedule serves
+ * renders of `rows` packed rows (owned rows of the tiling, <= 4096; others
+ * render in launch order) and is not thread-safe; one schedule per stream
+ * keeps each stream's measurements its own.  Create / destroy synchronise
+ * the device. */
+typedef struct sdf_schedule sdf_schedule;
+int sdf_schedule_create(int32_t rows, int32_t period, sdf_schedule** schedule);
+int sdf_schedule_destroy(sdf_schedule* schedule);
+/* The schedule's current order (blockIdx.y -> 8-row block) into order[0..n):
+ * returns the number of blocks it orders, 0 before its first cost snapshot
+ * has landed (launch order). */
+int sdf_schedule_order(const sdf_schedule* schedule, int32_t* order, int32_t n);
+int sdf_render_scheduled(const sdf_scene* scene, const sdf_camera* camera,
+                         const sdf_light* light, const sdf_material* material,
+                         const sdf_params* params, const sdf_tiling* tiling,
+                         void* rgba, int32_t* steps, sdf_schedule* schedule, void* stream);
+
 /* Scatter `nparts` packed row-block buffers (part r = rank r's output for
  * tiling {block_rows, r, nparts}), laid out back to back in `parts` with a
  * pitch of `part_stride_rows` rows each, into the full frame `frame`

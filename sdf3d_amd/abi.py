@@ -133,6 +133,12 @@ SIGNATURES = {
                                    C.c_int32, C.c_void_p, C.c_void_p]),
     "sdf_tiles_decode_tilings": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, _P(sdf_tiling),
                                            C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "sdf_schedule_create": (C.c_int, [C.c_int32, C.c_int32, _P(C.c_void_p)]),
+    "sdf_schedule_destroy": (C.c_int, [C.c_void_p]),
+    "sdf_schedule_order": (C.c_int, [C.c_void_p, _P(C.c_int32), C.c_int32]),
+    "sdf_render_scheduled": (C.c_int, [_P(sdf_scene), _P(sdf_camera), _P(sdf_light),
+                                       _P(sdf_material), _P(sdf_params), _P(sdf_tiling),
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sdf_tiles_decode_checked": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, _P(sdf_tiling),
                                            _P(C.c_int64), C.c_int32, C.c_int32, C.c_void_p,
                                            C.c_void_p, C.c_void_p]),
@@ -195,6 +201,8 @@ def load_library(path: Path | str | None = None, any_version: bool = False) -> C
             "There is no CPU fallback on the product path.")
     lib = C.CDLL(str(p))
     for name, (res, args) in SIGNATURES.items():
+        if any_version and not hasattr(lib, name):
+            continue   # an older build without a later entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -108,6 +108,45 @@ __device__ __forceinline__ float div_prepared(float a, float b, float yb) {
   return __builtin_fmaf(r, yb, q);
 }
 
+// (a0, a1, a2) / l with ONE reciprocal (normalize's three divisions): from y
+// = RN(1/l) (rcp_fast), q = RN(a y) is within 1.5 ulp of a/l; one Markstein
+// step (residual l q - a exact by FMA) makes it faithful, a second one
+// correctly rounded (Markstein's theorem needs q within 1 ulp, so one step
+// alone is no proof).  The residual's sign convention keeps a signed zero
+// numerator's sign.  Domain: l in [2^-30, 2^30), every a zero or |a| >=
+// 2^-60 (quotients and residuals stay normal); other lanes of the wave take
+// the IEEE division.
+__device__ __forceinline__ float div_refined(float a, float l, float y) {
+  float q = a * y;
+  float r = __builtin_fmaf(l, q, -a);
+  q = __builtin_fmaf(-r, y, q);
+  r = __builtin_fmaf(l, q, -a);
+  return __builtin_fmaf(-r, y, q);
+}
+__device__ __forceinline__ bool div3_ok(float a0, float a1, float a2, float l) {
+  // |a| bits shifted out of the sign; zero wraps to the top when 1 is subtracted
+  const uint32_t m = min(min((__float_as_uint(a0) << 1) - 1u, (__float_as_uint(a1) << 1) - 1u),
+                         (__float_as_uint(a2) << 1) - 1u);
+  return (__float_as_uint(l) - 0x30800000u) < (0x4E800000u - 0x30800000u) &&
+         m >= (0x21800000u << 1) - 1u;
+}
+__device__ __forceinline__ void div3(float& a0, float& a1, float& a2, float l) {
+  const float y = rcp_fast(l);
+  const bool ok = div3_ok(a0, a1, a2, l);
+  float q0 = div_refined(a0, l, y), q1 = div_refined(a1, l, y), q2 = div_refined(a2, l, y);
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+    if (!ok) {
+      q0 = a0 / l;
+      q1 = a1 / l;
+      q2 = a2 / l;
+    }
+  }
+  a0 = q0;
+  a1 = q1;
+  a2 = q2;
+}
+
 // n / k for the smooth-min (n in [0, k], any positive finite k), from the
 // host-prepared sc = 2^s with k sc in [2^-22, 2) (s <= 127) and ys =
 // RN(1/(k sc)): n/k = (n sc)/(k sc) exactly, k sc is exact, n sc is exact

@@ -23,7 +23,20 @@ struct RenderPlan {
   int rows;                // 0: nothing to render
   int tiles_ntiles;        // > 0: TILES output, compacted after the render
   uint32_t* tiles_used = nullptr;   // TILES: also receives the stream's length (device)
+  RowOrder order{};        // dispatch order of the 8-row blocks (a Schedule's; n = 0: none)
 };
+
+// A render schedule (sdf_schedule): the dispatch order of a plan's 8-row
+// blocks from the cost the kernels measured for them in earlier frames.
+struct Schedule;
+Schedule* schedule_create(int rows, int period);
+void schedule_destroy(Schedule* s);
+// before a launch: the latest order (once a cost snapshot has landed) into
+// plan->order, and the cost buffer the kernel adds to
+void schedule_apply(Schedule* s, RenderPlan* plan);
+// after the launch on `stream`: every `period` launches a snapshot of the
+// costs is copied to the host, behind the launch
+int schedule_after(Schedule* s, void* stream);
 
 // Rows a tiling owns (sdf_owned_rows), or SDF_E_INVALID_ARG.
 int count_rows(int height, const sdf_tiling& t);

@@ -11,6 +11,7 @@
 #include <stdint.h>
 #else
 typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint16_t uint16_t;
 typedef __hip_internal::uint32_t uint32_t;
 typedef __hip_internal::uint64_t uint64_t;
 #endif
@@ -67,6 +68,26 @@ struct KernelArgs {
   int32_t* steps;       // rows * width int2 or null
 };
 
+// ---- dispatch order of a frame's 8-row blocks (sdf_render_scheduled) -------
+// The render grid's row of workgroups blockIdx.y renders packed 8-row block
+// order[blockIdx.y] (n > 0; launch order otherwise): a schedule puts the
+// blocks that cost most in earlier frames first, so the frame's longest tiles
+// do not run alone at its end.  The table rides in the kernel-argument
+// segment (never a buffer another frame may be rewriting): any permutation
+// renders every block exactly once.  `cost` (may be null): each wave adds the
+// shader-clock cycles it took to its block's word.
+constexpr int kMaxOrderBlocks = 512;   // 4096 packed rows
+struct RowOrder {
+  unsigned long long* cost;
+  int32_t n;
+  int32_t reserved;
+  uint16_t order[kMaxOrderBlocks];
+};
+struct RenderArgs {
+  KernelArgs a;   // first: the kernels read it at the start of the segment
+  RowOrder o;
+};
+
 // Waves (8x8 tiles side by side) per render workgroup (render_kernel.inc
 // render / render_tiles; the built-in and the run-time specialised launchers).
 // Round 4: one wave per workgroup -- each wave is placed on its own, so the
@@ -110,6 +131,7 @@ struct FramesArgs {
 // raising kMaxAoTaps, SDF_MAX_PRIMS or kFramesPerLaunch fails here, not at launch
 static_assert(sizeof(FramesArgs) <= 4096, "FramesArgs exceeds the 4 KiB kernel-argument limit");
 static_assert(sizeof(KernelArgs) <= 4096, "KernelArgs exceeds the 4 KiB kernel-argument limit");
+static_assert(sizeof(RenderArgs) <= 4096, "RenderArgs exceeds the 4 KiB kernel-argument limit");
 // Tiles a wave takes per queue request, queues per launch (workgroup b uses
 // queue b % queues, i.e. one per XCD), and the queues' spacing in uint32s:
 // requests on one address serialise at the memory-side atomic unit, so the
@@ -122,16 +144,16 @@ constexpr int kQueueStride = 64;
 // Kernel launchers, one per precision translation unit (render_exact.hip /
 // render_fast.hip); `variant` selects a compile-time scene specialisation
 // (see render_kernel.inc).  Return a hipError_t as int.
-int launch_render_exact(const KernelArgs& a, int variant, void* stream);
-int launch_render_fast(const KernelArgs& a, int variant, void* stream);
+int launch_render_exact(const RenderArgs& a, int variant, void* stream);
+int launch_render_fast(const RenderArgs& a, int variant, void* stream);
 // the persistent frame-sequence kernel on `nblocks` 256-thread workgroups
 int launch_frames_exact(const FramesArgs& a, int variant, int nblocks, void* stream);
 int launch_frames_fast(const FramesArgs& a, int variant, int nblocks, void* stream);
 // the Mandelbulb scene's kernels live in units of their own
 // (render_{fast,exact}_bulb.hip, scheduled for ILP: sdf3d_amd/build.py); the
 // launchers above forward kVariantBulb to these
-int launch_render_exact_bulb(const KernelArgs& a, void* stream);
-int launch_render_fast_bulb(const KernelArgs& a, void* stream);
+int launch_render_exact_bulb(const RenderArgs& a, void* stream);
+int launch_render_fast_bulb(const RenderArgs& a, void* stream);
 int launch_frames_exact_bulb(const FramesArgs& a, int nblocks, void* stream);
 int launch_frames_fast_bulb(const FramesArgs& a, int nblocks, void* stream);
 int launch_deinterleave(const void* parts, int nparts, int part_stride_rows, int row_bytes,
@@ -203,7 +225,7 @@ __host__ __device__ inline uint32_t tile_qwords(uint32_t head) { return (head >>
 constexpr int kEscapeWindow = 12;   // base widths tried below the widest residual
 constexpr int kEscapeDwords = 72;   // bitstream bound: 3 width bytes + 3 x 12 x 63 bits
 // run-time specialised kernel for a scene signature (jit.cpp); -1 = none
-int launch_render_jit(const KernelArgs& a, const int* sig, int n, bool exact, void* stream);
+int launch_render_jit(const RenderArgs& a, const int* sig, int n, bool exact, void* stream);
 int jit_compiled_count();
 
 // ---- compile-time scene variants ------------------------------------------

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <initializer_list>
 #include <memory>
+#include <vector>
 
 #include "../../include/sdf_abi.h"
 #include "host_api.h"
@@ -451,20 +452,169 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
 int launch_render_plan(const RenderPlan& plan, void* stream) {
   if (plan.rows == 0) return SDF_OK;
   int err = -1;
-  if (plan.jit) err = launch_render_jit(plan.a, plan.sig, plan.nsig, plan.exact, stream);
+  RenderArgs r;
+  r.a = plan.a;
+  r.o.cost = plan.order.cost;
+  r.o.n = plan.order.n;
+  r.o.reserved = 0;
+  std::memcpy(r.o.order, plan.order.order, sizeof(uint16_t) * (size_t)std::max(plan.order.n, 0));
+  if (plan.jit) err = launch_render_jit(r, plan.sig, plan.nsig, plan.exact, stream);
   if (err == -1)
-    err = plan.exact ? launch_render_exact(plan.a, plan.variant, stream)
-                     : launch_render_fast(plan.a, plan.variant, stream);
+    err = plan.exact ? launch_render_exact(r, plan.variant, stream)
+                     : launch_render_fast(r, plan.variant, stream);
   if (err == hipSuccess && plan.tiles_ntiles > 0)
     err = launch_tiles_compact(plan.a.rgba, plan.tiles_ntiles, stream, plan.tiles_used);
   return err == hipSuccess ? SDF_OK : SDF_E_HIP;
 }
 
+// ---- render schedules (sdf_schedule) ---------------------------------------
+// The kernels add each wave's shader-clock cycles to its 8-row block's cost
+// word (RowOrder::cost).  Every `period` launches the schedule copies the
+// words to pinned host memory behind the launch; once such a copy has landed
+// (an event query: the host never waits), the cost of every block since the
+// previous snapshot orders the blocks for the next launches, costliest first
+// (LPT order: a frame's longest tiles start first, and short ones fill the
+// end of the frame instead of the longest ones running alone).  The order is
+// a permutation by construction and rides in the kernel arguments, so the
+// measurement is a heuristic only: every block is rendered exactly once
+// whatever the costs say.
+struct Schedule {
+  int rows = 0, nblocks = 0, period = 1;
+  int dev = 0;
+  unsigned long long* cost = nullptr;   // device, nblocks words (accumulating)
+  unsigned long long* snap = nullptr;   // pinned host, nblocks words
+  std::vector<unsigned long long> last; // the previous snapshot
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+  bool measure = false;                 // the launch being prepared measures its costs
+  long long launches = 0;
+  int n = 0;                            // 0 until the first order is known
+  std::vector<uint16_t> order;
+};
+
+Schedule* schedule_create(int rows, int period) {
+  auto* s = new Schedule();
+  s->rows = rows;
+  s->nblocks = (rows + 7) / 8;
+  s->period = period > 0 ? period : 1;
+  s->last.assign(s->nblocks, 0ull);
+  s->order.resize(s->nblocks);
+  bool ok = hipGetDevice(&s->dev) == hipSuccess && s->nblocks <= kMaxOrderBlocks;
+  const size_t bytes = sizeof(unsigned long long) * std::max(s->nblocks, 1);
+  ok = ok && hipMalloc((void**)&s->cost, bytes) == hipSuccess &&
+       hipMemset(s->cost, 0, bytes) == hipSuccess &&
+       hipHostMalloc((void**)&s->snap, bytes, hipHostMallocDefault) == hipSuccess &&
+       hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) == hipSuccess &&
+       hipDeviceSynchronize() == hipSuccess;
+  if (!ok) {
+    schedule_destroy(s);
+    return nullptr;
+  }
+  return s;
+}
+
+void schedule_destroy(Schedule* s) {
+  if (!s) return;
+  if (s->ev) {
+    (void)hipEventSynchronize(s->ev);
+    (void)hipEventDestroy(s->ev);
+  }
+  if (s->cost) (void)hipFree(s->cost);
+  if (s->snap) (void)hipHostFree(s->snap);
+  delete s;
+}
+
+void schedule_apply(Schedule* s, RenderPlan* plan) {
+  plan->order.n = 0;
+  plan->order.cost = nullptr;
+  if (!s || plan->rows != s->rows) return;   // another shape: launch order, no costs
+  if (s->pending && hipEventQuery(s->ev) == hipSuccess) {
+    s->pending = false;
+    std::vector<std::pair<unsigned long long, int>> d(s->nblocks);
+    unsigned long long total = 0;
+    for (int b = 0; b < s->nblocks; ++b) {
+      const unsigned long long v = s->snap[b] - s->last[b];
+      s->last[b] = s->snap[b];
+      d[b] = {v, b};
+      total += v;
+    }
+    if (total > 0) {
+      // costliest first; ties (and blocks not measured) in launch order
+      std::stable_sort(d.begin(), d.end(), [](const auto& x, const auto& y) {
+        return x.first > y.first;
+      });
+      for (int i = 0; i < s->nblocks; ++i) s->order[i] = (uint16_t)d[i].second;
+      s->n = s->nblocks;
+    }
+  }
+  // only the launch whose costs are copied out measures them (every wave's
+  // clock reads and its atomic add cost the others nothing)
+  s->measure = !s->pending && (s->launches % s->period) == 0;
+  plan->order.cost = s->measure ? s->cost : nullptr;
+  plan->order.n = s->n;
+  if (s->n) std::memcpy(plan->order.order, s->order.data(), sizeof(uint16_t) * s->n);
+}
+
+int schedule_after(Schedule* s, void* stream) {
+  if (!s) return SDF_OK;
+  s->launches++;
+  if (!s->measure) return SDF_OK;
+  s->measure = false;
+  if (hipMemcpyAsync(s->snap, s->cost, sizeof(unsigned long long) * s->nblocks,
+                     hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+      hipEventRecord(s->ev, (hipStream_t)stream) != hipSuccess)
+    return SDF_E_HIP;
+  s->pending = true;
+  return SDF_OK;
+}
+
 }  // namespace sdf
+
+struct sdf_schedule {
+  sdf::Schedule* s;
+};
 
 extern "C" {
 
 int sdf_abi_version(void) { return SDF_ABI_VERSION; }
+
+int sdf_schedule_create(int32_t rows, int32_t period, sdf_schedule** out) {
+  if (!out) return SDF_E_INVALID_ARG;
+  *out = nullptr;
+  if (rows <= 0 || rows > 8 * sdf::kMaxOrderBlocks || period < 1) return SDF_E_INVALID_ARG;
+  sdf::Schedule* s = sdf::schedule_create(rows, period);
+  if (!s) return SDF_E_HIP;
+  *out = new sdf_schedule{s};
+  return SDF_OK;
+}
+
+int sdf_schedule_destroy(sdf_schedule* s) {
+  if (!s) return SDF_OK;
+  sdf::schedule_destroy(s->s);
+  delete s;
+  return SDF_OK;
+}
+
+int sdf_schedule_order(const sdf_schedule* s, int32_t* order, int32_t n) {
+  if (!s || (n > 0 && !order)) return SDF_E_INVALID_ARG;
+  for (int i = 0; i < n && i < s->s->n; ++i) order[i] = s->s->order[i];
+  return s->s->n;
+}
+
+int sdf_render_scheduled(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
+                         const sdf_material* material, const sdf_params* params,
+                         const sdf_tiling* tiling, void* rgba, int32_t* steps,
+                         sdf_schedule* schedule, void* stream) {
+  sdf::RenderPlan plan;
+  int rc = sdf::make_render_plan(scene, camera, light, material, params, tiling, rgba, steps,
+                                 &plan);
+  if (rc != SDF_OK) return rc;
+  if (schedule) sdf::schedule_apply(schedule->s, &plan);
+  rc = sdf::launch_render_plan(plan, stream);
+  if (rc == SDF_OK && schedule && plan.rows == schedule->s->rows)
+    rc = sdf::schedule_after(schedule->s, stream);
+  return rc;
+}
 
 int sdf_defaults(sdf_scene* scene, sdf_camera* camera, sdf_light* light,
                  sdf_material* material, sdf_params* params, int32_t width, int32_t height) {

@@ -276,18 +276,23 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
         dl[ch] = __builtin_amdgcn_inverse_ballot_w64((uint64_t)mhi << 32 | mlo) ? d : 0u;
       }
       const uint32_t dw = (uint32_t)bs + (o >> 5);
-      // the window must lie in the tile's words (malformed masks or widths
-      // could point past them): such a lane loads nothing, the part is reported
-      const bool inside = dw + 2u < 2u * (uint32_t)nq;
-      if (__builtin_amdgcn_ballot_w64((dl[0] | dl[1] | dl[2]) && !inside)) report(kTilesBadField);
+      // this pixel's fields are bits [o, o + nb) of the bitstream: dwords dw
+      // .. dw + (endbit - 1) / 32, which must lie in the tile's words
+      // (malformed masks or widths could point past them: such a lane loads
+      // nothing, the part is reported); a load is made only for a dword the
+      // fields reach (the last tile's words may end the stream's buffer)
+      const uint32_t nb = dl[0] + dl[1] + dl[2];
+      const uint32_t endbit = (o & 31u) + nb;
+      const bool inside = nb == 0u || dw + ((endbit - 1u) >> 5) < 2u * (uint32_t)nq;
+      if (__builtin_amdgcn_ballot_w64(!inside)) report(kTilesBadField);
 #if SDF_DECODE_ESC_VMEM
       // dwords dw .. dw + 2 of the tile's data, loaded by the lanes with fields
       uint32_t d0 = 0u, d1 = 0u, d2 = 0u;
-      if ((dl[0] | dl[1] | dl[2]) && inside) {
+      if (nb && inside) {
         const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
         d0 = t32[dw];
-        d1 = t32[dw + 1];
-        d2 = t32[dw + 2];
+        d1 = endbit > 32u ? t32[dw + 1] : 0u;
+        d2 = endbit > 64u ? t32[dw + 2] : 0u;
       }
 #else
       // dwords dw .. dw + 2 of the tile's data: qwords dw / 2 and dw / 2 + 1
@@ -298,11 +303,11 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
       const uint32_t t0 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].x);
       const uint32_t t1 = __builtin_amdgcn_ds_bpermute(a + 4, (int)pa[k].y);
       uint32_t d0 = (dw & 1) ? s1 : s0, d1 = (dw & 1) ? t0 : s1, d2 = (dw & 1) ? t1 : t0;
-      if ((dl[0] | dl[1] | dl[2]) && dw + 2 >= 128 && inside) {   // beyond the loaded qwords: rare
+      if (nb && dw + 2 >= 128 && inside) {   // beyond the loaded qwords: rare
         const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tdata);
         d0 = t32[dw];
-        d1 = t32[dw + 1];
-        d2 = t32[dw + 2];
+        d1 = endbit > 32u ? t32[dw + 1] : 0u;
+        d2 = endbit > 64u ? t32[dw + 2] : 0u;
       }
 #endif
       f_lo = __builtin_amdgcn_alignbit(d1, d0, o & 31);

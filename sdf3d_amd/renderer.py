@@ -119,12 +119,19 @@ class Renderer:
               if steps else None)
         return rgba, st
 
+    def schedule(self, rows: int, period: int = 1) -> "Schedule":
+        """A render schedule for frames of `rows` packed rows (sdf_schedule):
+        pass it to ``render(..., schedule=)`` to dispatch the rows' 8-row
+        blocks costliest first (bit-identical output)."""
+        return Schedule(self, rows, period)
+
     def render(self, frame: Frame, t: abi.sdf_tiling | None = None, out=None,
-               steps=False, stream=None):
+               steps=False, stream=None, schedule: "Schedule | None" = None):
         """Render the rows owned by tiling `t` (None = whole frame).
 
         Returns (rgba[rows, W, 4] float32, steps[rows, W, 2] int32 or None), both
-        on the device, asynchronous on `stream` (default: torch's current)."""
+        on the device, asynchronous on `stream` (default: torch's current).
+        `schedule`: dispatch order of the row blocks (sdf_render_scheduled)."""
         torch = self.torch
         rows = buffer_rows(frame.params.height, t)
         w = frame.params.width
@@ -151,13 +158,15 @@ class Renderer:
                                or not st.is_contiguous()):
             raise ValueError(f"steps must be a contiguous int32 ({rows}, {w}, 2) tensor")
         with self._on_device():
-            rc = self.lib.sdf_render(
-                C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
-                C.byref(frame.material), C.byref(frame.params),
-                C.byref(t) if t is not None else None,
-                C.c_void_p(rgba.data_ptr()),
-                C.c_void_p(st.data_ptr()) if st is not None else None,
-                self._stream(stream))
+            args = (C.byref(frame.scene), C.byref(frame.camera), C.byref(frame.light),
+                    C.byref(frame.material), C.byref(frame.params),
+                    C.byref(t) if t is not None else None,
+                    C.c_void_p(rgba.data_ptr()),
+                    C.c_void_p(st.data_ptr()) if st is not None else None)
+            if schedule is None:
+                rc = self.lib.sdf_render(*args, self._stream(stream))
+            else:
+                rc = self.lib.sdf_render_scheduled(*args, schedule.handle, self._stream(stream))
         abi.check(rc, "sdf_render")
         return rgba, st
 
@@ -317,3 +326,35 @@ class Renderer:
                 None if status is None else C.c_void_p(status.data_ptr()), self._stream(stream))
         abi.check(rc, "sdf_tiles_decode_checked")
         return out, status
+
+
+class Schedule:
+    """sdf_schedule: the dispatch order of a frame's 8-row blocks, costliest
+    first, learnt from the cycles the kernels measured in earlier frames
+    (include/sdf_abi.h).  One per stream; ``close()`` frees it."""
+
+    def __init__(self, renderer: "Renderer", rows: int, period: int = 1):
+        self.lib = renderer.lib
+        self.handle = C.c_void_p()
+        with renderer._on_device():
+            abi.check(self.lib.sdf_schedule_create(int(rows), int(period), C.byref(self.handle)),
+                      "sdf_schedule_create")
+
+    def order(self) -> list[int]:
+        """blockIdx.y -> 8-row block ([] until the first cost snapshot landed)."""
+        buf = (C.c_int32 * 512)()
+        n = self.lib.sdf_schedule_order(self.handle, buf, 512)
+        if n < 0:
+            abi.check(n, "sdf_schedule_order")
+        return list(buf[:n])
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.sdf_schedule_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
