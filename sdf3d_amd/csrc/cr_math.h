@@ -123,12 +123,53 @@ __device__ __forceinline__ float div_refined(float a, float l, float y) {
   r = __builtin_fmaf(l, q, -a);
   return __builtin_fmaf(-r, y, q);
 }
-__device__ __forceinline__ bool div3_ok(float a0, float a1, float a2, float l) {
-  // |a| bits shifted out of the sign; zero wraps to the top when 1 is subtracted
+// the divisor's magnitude in [2^-30, 2^30) (either sign)
+__device__ __forceinline__ bool divisor_ok(float l) {
+  return ((__float_as_uint(l) << 1) - (0x30800000u << 1)) < ((0x4E800000u - 0x30800000u) << 1);
+}
+// every numerator zero or of magnitude >= 2^-60 (|a| bits shifted out of the
+// sign; a zero wraps to the top when 1 is subtracted).  The callers' own
+// domains bound |a| above: |a| <= l (normalize), the working range (the
+// Mandelbulb's p - c).
+__device__ __forceinline__ bool numerators_ok(float a0, float a1, float a2) {
   const uint32_t m = min(min((__float_as_uint(a0) << 1) - 1u, (__float_as_uint(a1) << 1) - 1u),
                          (__float_as_uint(a2) << 1) - 1u);
-  return (__float_as_uint(l) - 0x30800000u) < (0x4E800000u - 0x30800000u) &&
-         m >= (0x21800000u << 1) - 1u;
+  return m >= (0x21800000u << 1) - 1u;
+}
+__device__ __forceinline__ bool div3_ok(float a0, float a1, float a2, float l) {
+  return divisor_ok(l) && numerators_ok(a0, a1, a2);
+}
+// (a0, a1, a2) / l from the host's y = RN(1/l), l's range checked by the
+// caller (wave-uniform): the Mandelbulb's (p - c) / scale
+__device__ __forceinline__ void div3_prepared(float& a0, float& a1, float& a2, float l, float y) {
+  const bool ok = numerators_ok(a0, a1, a2);
+  float q0 = div_refined(a0, l, y), q1 = div_refined(a1, l, y), q2 = div_refined(a2, l, y);
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+    if (!ok) {
+      q0 = a0 / l;
+      q1 = a1 / l;
+      q2 = a2 / l;
+    }
+  }
+  a0 = q0;
+  a1 = q1;
+  a2 = q2;
+}
+// a / b for one division (the DE's, the shadow march's): y = RN(1/b) by
+// rcp_fast (also exact for negative b: every step is odd-symmetric), two
+// Markstein steps; |b| in [2^-30, 2^30) and a zero or |a| in [2^-60, 2^60)
+// (guarded; the IEEE division elsewhere)
+__device__ __forceinline__ float div_one(float a, float b) {
+  const uint32_t ua = (__float_as_uint(a) << 1) - 1u;
+  const bool ok = divisor_ok(b) && ua >= (0x21800000u << 1) - 1u &&
+                  (ua < (0x5D800000u << 1) - 1u || ua == 0xFFFFFFFFu);
+  float q = div_refined(a, b, rcp_fast(b));
+  if (any_lane(!ok)) {
+    SDF_CRM_COLD();
+    if (!ok) q = a / b;
+  }
+  return q;
 }
 __device__ __forceinline__ void div3(float& a0, float& a1, float& a2, float l) {
   const float y = rcp_fast(l);

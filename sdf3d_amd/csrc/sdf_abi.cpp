@@ -775,6 +775,12 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   if (!invert_view(camera->view, inv)) return SDF_E_INVALID_ARG;
   for (float v : inv)
     if (!(std::fabs(v) <= kMaxCoord)) return SDF_E_INVALID_ARG;
+  // the hoisted camera position inverse(V_mat) * (eye, 1) (voxel_fragment.frag:180)
+  for (int i = 0; i < 3; ++i) {
+    const double c = (double)inv[i] * camera->eye[0] + (double)inv[4 + i] * camera->eye[1] +
+                     (double)inv[8 + i] * camera->eye[2] + inv[12 + i];
+    if (!(std::fabs(c) <= kMaxCoord)) return SDF_E_INVALID_ARG;
+  }
   for (int i = 0; i < 3; ++i)
     if (std::fabs(camera->eye[i]) > kMaxCoord || std::fabs(light->pos[i]) > kMaxCoord)
       return SDF_E_INVALID_ARG;

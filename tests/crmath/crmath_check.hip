@@ -14,6 +14,9 @@
 //          2^-100)
 //   minmax : v_min_f32 / v_max_f32 vs the GLSL select on the operand pairs
 //          the exact kernel relies on (hw_min / hw_max)
+//   rcpneg : rcp_fast on the negative half of its domain
+//   div  : the Markstein divisions (div_one / div_refined) vs IEEE a / b on
+//          2^32 sampled pairs (edge families included)
 //   pow  : shade.h spec_pow<exact>(x, n) (repeated squaring in fp64, the
 //          library pow on lanes near a rounding boundary) vs the library
 //          (float)pow((double)x, (double)n), for EVERY float x in [0, 1.0001]
@@ -208,6 +211,73 @@ __global__ void check_pow(unsigned base, Counts* c) {
   tally(c, bad_n != 0ull, true, bad_n != 0ull, u);
 }
 
+// rcp_fast on the negative half of its domain: -[2^-100, 2^100) (the
+// shadow march's divisor 2 h_prev may be negative)
+__global__ void check_rcp_neg(unsigned base, Counts* c) {
+  const unsigned u = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const float x = -__uint_as_float(u);
+  const bool in = sdf::crm::sqrt_fast_ok(-x);
+  const float a = sdf::crm::rcp_fast(x), b = 1.0f / x;
+  const bool bad = in && !same_bits(a, b);
+  tally(c, bad, in, bad, u);
+}
+
+// Markstein divisions (cr_math.h div_refined / div_one; render_kernel.inc
+// normalize, the Mandelbulb's (p - c) / scale, its DE, the shadow march):
+// 2^32 sampled (a, b) pairs, b of magnitude log-uniform over [2^-30, 2^30)
+// (either sign) plus out-of-range b, a from four families: |a| <= |b|
+// (normalize), any magnitude in [2^-60, 2^60), quotients within a few ulps of
+// a power of two or of 1 (hard rounding cases), and zeros, denormals, tiny
+// and huge a (the guard's edges).  "mismatch": div_one (guard included) vs
+// IEEE a / b on every pair; "effective": the unguarded two-step quotient vs
+// IEEE on the pairs inside the guard ("fast_path" counts those).
+__global__ void check_div(unsigned base, Counts* c) {
+  const unsigned i = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned fam = i >> 30;
+  const unsigned h1 = hash32(i * 2654435761u + 99u), h2 = hash32(h1 ^ 0x5bd1e995u),
+                 h3 = hash32(h2 + i);
+  // b: exponent in [-30, 29] (1 in 64: [-40, 40], partly outside), random sign
+  const int eb = (h1 & 63u) == 0u ? (int)(h1 >> 6) % 81 - 40 : (int)((h1 >> 6) % 60u) - 30;
+  float b = __builtin_ldexpf(__uint_as_float(0x3F800000u | (h2 & 0x7FFFFFu)), eb);
+  if (h2 & 0x80000000u) b = -b;
+  float a;
+  switch (fam) {
+    case 0:   // |a| <= |b| (normalize's components)
+      a = b * (2.0f * __uint_as_float(0x3F800000u | (h3 >> 9)) - 3.0f);
+      break;
+    case 1: {  // any magnitude 2^-60 .. 2^60
+      const int ea = (int)(h3 % 120u) - 60;
+      a = __builtin_ldexpf(__uint_as_float(0x3F800000u | (hash32(h3) & 0x7FFFFFu)), ea);
+      if (h3 & 1u) a = -a;
+      break;
+    }
+    case 2: {  // a = b * (2^k +- a few ulps): quotients near powers of two
+      const int k = (int)(h3 % 41u) - 20;
+      const float t = __builtin_ldexpf(1.0f, k);
+      const int d = (int)(hash32(h3) % 9u) - 4;
+      a = b * __uint_as_float(__float_as_uint(t) + (unsigned)d);
+      break;
+    }
+    default: {  // edges: +-0, denormals, tiny, huge, just inside / outside the guard
+      const unsigned sel = h3 % 8u;
+      const unsigned r = hash32(h3);
+      a = sel == 0 ? 0.0f : sel == 1 ? -0.0f : sel == 2 ? __uint_as_float(r & 0x007FFFFFu)
+        : sel == 3 ? __builtin_ldexpf(1.0f + (r >> 9) * 0x1p-23f, -61 + (int)(r % 4u))
+        : sel == 4 ? __builtin_ldexpf(1.0f + (r >> 9) * 0x1p-23f, 58 + (int)(r % 4u))
+        : sel == 5 ? __uint_as_float(0x3F800000u | (r >> 9)) * 1e30f
+        : sel == 6 ? __builtin_ldexpf(1.0f, -60) : -__builtin_ldexpf(1.0f, 60) * 0.999f;
+      break;
+    }
+  }
+  const float ieee = a / b;
+  const bool bad = !same_bits(sdf::crm::div_one(a, b), ieee);
+  const uint32_t ua = (__float_as_uint(a) << 1) - 1u;
+  const bool in = sdf::crm::divisor_ok(b) && ua >= (0x21800000u << 1) - 1u &&
+                  (ua < (0x5D800000u << 1) - 1u || ua == 0xFFFFFFFFu);
+  const bool eff = in && !same_bits(sdf::crm::div_refined(a, b, sdf::crm::rcp_fast(b)), ieee);
+  tally(c, bad, in, eff, i);
+}
+
 static int run(const char* name, void (*kern)(unsigned, Counts*), Counts* d, char* out,
                size_t cap, unsigned long long end = 1ull << 32) {
   (void)hipMemset(d, 0, sizeof(Counts));
@@ -241,7 +311,8 @@ int main(int argc, char** argv) {
   } checks[] = {{"rcp", check_rcp, 1ull << 32, ""},   {"sqrt", check_sqrt, 1ull << 32, ""},
                 {"log", check_log, 1ull << 32, ""},   {"smin", check_smin, 1ull << 32, ""},
                 {"sminedge", check_smin_edges, 1ull << 32, ""},
-                {"pow", check_pow, kPowXEnd, ""}, {"minmax", check_minmax, 256, ""}};
+                {"pow", check_pow, kPowXEnd, ""}, {"minmax", check_minmax, 256, ""},
+                {"rcpneg", check_rcp_neg, 1ull << 32, ""}, {"div", check_div, 1ull << 32, ""}};
   // an argument selects checks by name (e.g. "sqrt,log"; "smin" matches only
   // itself)
   auto wanted = [&](const char* name) {

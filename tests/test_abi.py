@@ -270,3 +270,19 @@ def test_validate_rejects_degenerate_capsule():
     for j in range(3):
         pr.p[3 + j] = pr.p[j]
     assert _validate(f) == abi.SDF_E_INVALID_ARG
+
+
+def test_schedule_and_checked_decode_refuse_bad_arguments():
+    """Host-side argument checks of the round-5 entry points (no device)."""
+    lib = abi.load_library()
+    h = C.c_void_p()
+    for rows, period in [(0, 1), (-8, 1), (4097, 1), (64, 0)]:
+        assert lib.sdf_schedule_create(rows, period, C.byref(h)) == abi.SDF_E_INVALID_ARG
+        assert not h.value
+    assert lib.sdf_schedule_create(64, 1, None) == abi.SDF_E_INVALID_ARG
+    assert lib.sdf_schedule_destroy(None) == abi.SDF_OK
+    assert lib.sdf_schedule_order(None, None, 0) == abi.SDF_E_INVALID_ARG
+    t = (abi.sdf_tiling * 1)()
+    for nparts in (0, abi.MAX_DECODE_PARTS + 1):
+        assert lib.sdf_tiles_decode_checked(None, nparts, 0, t, None, 8, 8, None, None,
+                                            None) == abi.SDF_E_INVALID_ARG

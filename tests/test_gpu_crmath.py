@@ -82,3 +82,19 @@ def test_hardware_min_max_equal_the_select_where_used(results):
     pairs those proofs rest on are checked on the hardware."""
     r = results["minmax"]
     assert r["mismatch"] == 0 and r["fast_path"] == 22, r
+
+
+def test_rcp_fast_negative_half(results):
+    r = results["rcpneg"]
+    assert r["fast_path"] == 200 * 2**23 and r["mismatch"] == 0, r
+
+
+def test_markstein_divisions_are_ieee(results):
+    """normalize / the Mandelbulb's divisions / the shadow march's division
+    by one reciprocal and two Markstein steps (cr_math.h div_one,
+    div_refined): bit-identical to IEEE a / b on 2^32 sampled pairs, inside
+    the guard by the two steps themselves ("effective" 0), everywhere with the
+    guard's fall-back ("mismatch" 0)."""
+    r = results["div"]
+    assert r["inputs"] == 2**32 and r["mismatch"] == 0 and r["effective"] == 0, r
+    assert r["fast_path"] > 0.7 * 2**32, r

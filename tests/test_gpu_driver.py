@@ -128,10 +128,15 @@ def test_frame_not_shipped_is_refused(nccl_world1):
     assert torch.equal(got.view(torch.int32), _reference(f).view(torch.int32))
 
 
-@pytest.mark.parametrize("nproc,cfg,shares,batch,streams,nonblocking", [
-    (2, "C3", None, 2, 4, True), (3, "C3", "1:2", 1, 4, False), (3, "C3", None, 4, 8, True),
-    (8, "C3", None, 4, 8, False), (8, "C4", None, 0, 0, False)])
-def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, nonblocking):
+@pytest.mark.parametrize("nproc,cfg,shares,batch,streams,nonblocking,lag", [
+    (2, "C3", None, 2, 4, True, 0), (3, "C3", "1:2", 1, 4, False, 0),
+    (3, "C3", None, 4, 8, True, 0), (8, "C3", None, 4, 8, False, 0),
+    (8, "C4", None, 0, 0, False, 0),
+    # 16 buffer sets on the driver's 4 render streams, batches of
+    # 8 shipped 8 frames late -- buffer sets share streams, and their waits
+    # must not form a cycle across ranks
+    (3, "C3", None, 8, 16, False, 8), (2, "C5", None, 8, 16, True, 8)])
+def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, nonblocking, lag):
     """The native C++ driver's multi-rank sequence (render, RCCL-style length
     all-gather, send/recv of the TILES streams to rank 0, decode) with
     `nproc` ranks sharing this GPU: bench.py --driver native over the
@@ -161,6 +166,7 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, n
              "--config", cfg, "--no-display", "--clock-warm-s", "0"]
         c += ["--batch", str(batch)] if batch else []
         c += ["--streams", str(streams)] if streams else []
+        c += ["--lag", str(lag), "--steps", "20"] if lag else []
         return c + (["--shares", shares] if shares else [])
     env = dict(os.environ, SHMCOMM_TIMEOUT_MS="60000", GPU_MAX_HW_QUEUES="8",
                SHMCOMM_REQUIRE_ASYNC="1", SHMCOMM_STATS="1")
