@@ -156,15 +156,18 @@ __device__ __forceinline__ void div3_prepared(float& a0, float& a1, float& a2, f
   a1 = q1;
   a2 = q2;
 }
-// a / b for one division (the DE's, the shadow march's): y = RN(1/b) by
-// rcp_fast (also exact for negative b: every step is odd-symmetric), two
-// Markstein steps; |b| in [2^-30, 2^30) and a zero or |a| in [2^-60, 2^60)
-// (guarded; the IEEE division elsewhere)
+// a / b for one division (the DE's, the shadow march's): computed as
+// (sign(b) a) / |b| -- the same correctly rounded quotient (round to nearest
+// is symmetric), and with a positive divisor the two steps keep a zero
+// numerator's sign (with a negative one +0 / b would come out +0, not -0) --
+// y = RN(1/|b|) by rcp_fast, two Markstein steps; |b| in [2^-30, 2^30) and a
+// zero or |a| in [2^-60, 2^60) (guarded; the IEEE division elsewhere)
 __device__ __forceinline__ float div_one(float a, float b) {
   const uint32_t ua = (__float_as_uint(a) << 1) - 1u;
   const bool ok = divisor_ok(b) && ua >= (0x21800000u << 1) - 1u &&
                   (ua < (0x5D800000u << 1) - 1u || ua == 0xFFFFFFFFu);
-  float q = div_refined(a, b, rcp_fast(b));
+  const float mb = __builtin_fabsf(b);
+  float q = div_refined(__builtin_copysignf(1.0f, b) * a, mb, rcp_fast(mb));
   if (any_lane(!ok)) {
     SDF_CRM_COLD();
     if (!ok) q = a / b;

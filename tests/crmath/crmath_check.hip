@@ -274,7 +274,10 @@ __global__ void check_div(unsigned base, Counts* c) {
   const uint32_t ua = (__float_as_uint(a) << 1) - 1u;
   const bool in = sdf::crm::divisor_ok(b) && ua >= (0x21800000u << 1) - 1u &&
                   (ua < (0x5D800000u << 1) - 1u || ua == 0xFFFFFFFFu);
-  const bool eff = in && !same_bits(sdf::crm::div_refined(a, b, sdf::crm::rcp_fast(b)), ieee);
+  const float mb = __builtin_fabsf(b);
+  const bool eff = in && !same_bits(sdf::crm::div_refined(__builtin_copysignf(1.0f, b) * a, mb,
+                                                          sdf::crm::rcp_fast(mb)),
+                                    ieee);
   tally(c, bad, in, eff, i);
 }
 

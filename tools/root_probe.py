@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--config", default="C4")
+    ap.add_argument("--precision", default="fast", choices=["fast", "exact"])
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--shares", default="1:1", help="rank 0 : other ranks, blocks per period")
     ap.add_argument("--streams", type=int, default=3, help="alternating streams / buffers")
@@ -49,7 +50,8 @@ def main():
     if args.lib:
         rd.lib = abi.load_library(args.lib, any_version=True)
     N, K = args.world, args.frames
-    f = scenes.config(args.config, precision=abi.PRECISION_FAST)
+    f = scenes.config(args.config, precision=abi.PRECISION_FAST if args.precision == "fast"
+                      else abi.PRECISION_EXACT)
     W, H = f.params.width, f.params.height
     ft = f.copy()
     ft.params.output_format = abi.FORMAT_TILES
@@ -113,7 +115,7 @@ def main():
         torch.cuda.synchronize()
         return round((time.perf_counter() - t0) / K * 1e3, 4)
 
-    out = {"config": args.config, "world": N, "shares": args.shares, "frames": K, "streams": NS}
+    out = {"config": args.config, "precision": args.precision, "world": N, "shares": args.shares, "frames": K, "streams": NS}
     if args.only:
         leg = {"decode": dict(render=False), "root": dict(), "peer": dict(render=False,
                decode=False, peer=True),

@@ -35,12 +35,14 @@ def build() -> Path:
     return EXE
 
 
-def write_frame(path: Path, cfg: str, world: int, a: int, b: int, sets: int) -> None:
+def write_frame(path: Path, cfg: str, world: int, a: int, b: int, sets: int,
+                precision: str = "fast") -> None:
     from sdf3d_amd import abi, scenes
-    f = scenes.config(cfg, precision=abi.PRECISION_FAST)
+    prec = abi.PRECISION_FAST if precision == "fast" else abi.PRECISION_EXACT
+    f = scenes.config(cfg, precision=prec)
     cams = []
     for s in range(sets):
-        g = scenes.config(cfg, precision=abi.PRECISION_FAST, pose=s % len(scenes.POSES))
+        g = scenes.config(cfg, precision=prec, pose=s % len(scenes.POSES))
         if s >= len(scenes.POSES):   # more sets than poses: small extra yaw
             scenes.set_view(g, scenes.orbit_view(*scenes.POSES[s % len(scenes.POSES)])
                             @ scenes.orbit_view(3.0 * (s // len(scenes.POSES)), 0.0))
@@ -53,6 +55,7 @@ def write_frame(path: Path, cfg: str, world: int, a: int, b: int, sets: int) -> 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C4")
+    ap.add_argument("--precision", default="fast", choices=["fast", "exact"])
     ap.add_argument("--worlds", default="8:2:7", help="world:a:b,...")
     ap.add_argument("--batches", default="2")
     ap.add_argument("--sets", type=int, default=4)
@@ -76,7 +79,7 @@ def main():
     for spec in args.worlds.split(","):
         world, a, b = (int(v) for v in spec.split(":"))
         fb = out_dir / f"rccl_probe_{world}.bin"
-        write_frame(fb, args.config, world, a, b, args.sets)
+        write_frame(fb, args.config, world, a, b, args.sets, args.precision)
         for batch, mode in [(int(v), m) for v in args.batches.split(",")
                             for m in args.modes.split(",")]:
             r = subprocess.run([str(exe), str(fb), rccl, str(args.frames), str(args.warmup),
@@ -86,6 +89,7 @@ def main():
             d = json.loads(line[-1]) if line else {"error": r.stderr[-2000:]}
             d["rc"] = r.returncode
             d["config"] = args.config
+            d["precision"] = args.precision
             res.append(d)
             print(json.dumps(d), flush=True)
             if r.returncode != 0:
