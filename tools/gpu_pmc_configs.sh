@@ -1,5 +1,15 @@
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-for c in C4 C5 C2; do
-  timeout -k 10 400 python tools/pmc_traffic.py --config $c --precision fast --out gpurun_out/pmc > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed rc=$?"; exit 1; }
-  echo "pmc $c ok"
+#!/bin/bash
+# PMC summaries (tools/pmc_traffic.py: one rocprofv3 --pmc pass per counter
+# set, no tracing domains) for SPECS = "config:precision ..." ->
+# gpurun_out/pmc/pmc_<cfg>_<prec>.json (copy into profiles/ to commit).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for spec in ${SPECS:-C4:exact C4:fast}; do
+  IFS=: read -r c p <<< "$spec"
+  timeout -k 10 400 python tools/pmc_traffic.py --config $c --precision $p --out gpurun_out/pmc \
+    > gpurun_out/pmc_${c}_$p.log 2>&1
+  rc=$?; echo "pmc $c $p rc=$rc"
+  [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc_${c}_$p.log; exit $rc; }
 done
+exit 0
