@@ -3,11 +3,13 @@
 // sequences yet bit-identical to what the oracle computes (IEEE sqrtf, a / b,
 // and log evaluated in fp64 and rounded once: oracle/sdf_oracle.c cr_logf).
 //
-//   cr_sqrt(x)           == sqrtf(x) for every x.  Fast path on [2^-100,
-//                           2^100): v_rsq, then one Newton/Markstein
-//                           correction (rsq, 2 mul, 2 fma) instead of the
-//                           generic v_sqrt + denormal scaling + 2-candidate
-//                           residual test + class fix-up (17 instructions).
+//   cr_sqrt(x)           == sqrtf(x) for every x (every x but +INF with
+//                           SDF_CRM_SQRT_GUARD 1).  Fast path on [2^-100,
+//                           2^100) (on [2^-100, FLT_MAX] with guard 1): v_rsq,
+//                           then one Newton/Markstein correction (rsq, 2 mul,
+//                           2 fma) instead of the generic v_sqrt + denormal
+//                           scaling + 2-candidate residual test + class
+//                           fix-up (17 instructions).
 //   div_prepared(a,b,yb) == a / b, given yb = RN(1/b) prepared on the host,
 //                           by Markstein's theorem (q within 1 ulp, r exact,
 //                           fma(r, yb, q) = RN(a/b)) wherever a/b, q and r
@@ -52,9 +54,28 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 
 // x in [2^-100, 2^100) (positive, normal, far from both ends of the range):
 // the fast path's x * y, s * s and residual neither underflow nor overflow
+// (the domain rcp_fast is checked on, tests/crmath/crmath_check.hip)
 __device__ __forceinline__ bool sqrt_fast_ok(float x) {
   return (__float_as_uint(x) - 0x0D800000u) < (0x71800000u - 0x0D800000u);
 }
+
+// The guard cr_sqrt takes the fast path behind (SDF_CRM_SQRT_GUARD):
+//   0  the integer range test above (2 VALU): cr_sqrt(x) == sqrtf(x) for
+//      EVERY x.
+//   1  ONE float compare, x >= 2^-100 (catches 0, denormals, tiny x,
+//      negatives and NaN): the fast path is exact on all of [2^-100,
+//      FLT_MAX] (tests/crmath "sqrtwide", every positive normal), so
+//      cr_sqrt(x) == sqrtf(x) for every x but +INF (where it gives NaN).
+//      For callers whose arguments are finite by their domain:
+//      render_kernel.inc sets it for the CSG units, where sdf_validate's
+//      working range bounds every squared length far below FLT_MAX; the
+//      Mandelbulb unit keeps 0 (its orbit may overflow).
+// (A guard on the fast path's own product x RN(1/sqrt x) >= 2^-50 -- also
+// one compare -- fails: v_rsq flushes denormal inputs to +-INF, and x * INF
+// passes it.  tests/crmath "sqrt" caught that.)
+#ifndef SDF_CRM_SQRT_GUARD
+#define SDF_CRM_SQRT_GUARD 0
+#endif
 
 __device__ __forceinline__ float sqrt_fast(float x) {
   const float y = __builtin_amdgcn_rsqf(x);   // 1/sqrt(x), ~1 ulp
@@ -63,31 +84,39 @@ __device__ __forceinline__ float sqrt_fast(float x) {
   const float r = __builtin_fmaf(-s, s, x);   // x - s^2, exact
   return __builtin_fmaf(h, r, s);
 }
+template <int G>
+__device__ __forceinline__ bool sqrt_guard_g(float x) {
+  if constexpr (G == 1) return x >= 0x1p-100f;
+  else return sqrt_fast_ok(x);
+}
+__device__ __forceinline__ bool sqrt_guard(float x) { return sqrt_guard_g<SDF_CRM_SQRT_GUARD>(x); }
 
-__device__ __forceinline__ float cr_sqrt(float x) {
+template <int G>
+__device__ __forceinline__ float cr_sqrt_g(float x) {
   float s = sqrt_fast(x);
-  const bool ok = sqrt_fast_ok(x);
+  const bool ok = sqrt_guard_g<G>(x);
   if (any_lane(!ok)) {
     SDF_CRM_COLD();
     s = ok ? s : __builtin_sqrtf(x);
   }
   return s;
 }
+__device__ __forceinline__ float cr_sqrt(float x) { return cr_sqrt_g<SDF_CRM_SQRT_GUARD>(x); }
 
 // N square roots behind ONE guard (independent chains stay in one basic
-// block, render_kernel.inc mandelbulb_n): each s[i] == sqrtf(x[i])
+// block, render_kernel.inc mandelbulb_n): each s[i] == cr_sqrt(x[i])
 template <int N>
 __device__ __forceinline__ void cr_sqrt_n(const float (&x)[N], float (&s)[N]) {
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < N; i++) {
     s[i] = sqrt_fast(x[i]);
-    ok = ok & sqrt_fast_ok(x[i]);
+    ok = ok & sqrt_guard(x[i]);
   }
   if (any_lane(!ok)) {
     SDF_CRM_COLD();
 #pragma unroll
-    for (int i = 0; i < N; i++) s[i] = sqrt_fast_ok(x[i]) ? s[i] : __builtin_sqrtf(x[i]);
+    for (int i = 0; i < N; i++) s[i] = sqrt_guard(x[i]) ? s[i] : __builtin_sqrtf(x[i]);
   }
 }
 
@@ -137,7 +166,10 @@ __device__ __forceinline__ bool numerators_ok(float a0, float a1, float a2) {
   return m >= (0x21800000u << 1) - 1u;
 }
 __device__ __forceinline__ bool div3_ok(float a0, float a1, float a2, float l) {
-  return divisor_ok(l) && numerators_ok(a0, a1, a2);
+  // `&`, not `&&`: no short-circuit branch (which made the compiler carry the
+  // mask across blocks and rebuild it with v_cndmask + v_cmp)
+  const bool d = divisor_ok(l), n = numerators_ok(a0, a1, a2);
+  return d & n;
 }
 // (a0, a1, a2) / l from the host's y = RN(1/l), l's range checked by the
 // caller (wave-uniform): the Mandelbulb's (p - c) / scale

@@ -2,6 +2,13 @@
 // exact-precision kernel's correctly rounded building blocks
 // (sdf3d_amd/csrc/cr_math.h) against the generic sequences they replace:
 //   sqrt : cr_sqrt(x) vs IEEE sqrtf(x) on all 2^32 bit patterns
+//   sqrtbounded : cr_sqrt with the one-compare guard (SDF_CRM_SQRT_GUARD 1)
+//          vs sqrtf on all 2^32 bit patterns: "effective" counts mismatches
+//          other than x = +INF (the one input it does not cover)
+//   sqrtwide : the unguarded sqrt_fast(x) vs sqrtf(x) on EVERY positive normal
+//          x (v_cmp_class's "positive normal"): "mismatch" counts them all,
+//          "effective" those below 2^-100 (the range a class-only guard would
+//          add at the bottom; the top, 2^100 .. FLT_MAX, is the rest)
 //   rcp  : rcp_fast(x) vs IEEE 1.0f / x on its domain [2^-100, 2^100)
 //   log  : cr_log(x) vs (float)log((double)x) on all 2^32 bit patterns
 //   smin : div_scaled(n, k, sc, ys) vs n / k over the smooth-min domain
@@ -61,7 +68,24 @@ __global__ void check_sqrt(unsigned base, Counts* c) {
   const float x = __uint_as_float(u);
   const float a = sdf::crm::cr_sqrt(x), b = __builtin_sqrtf(x);
   const bool bad = !same_bits(a, b);
-  tally(c, bad, sdf::crm::sqrt_fast_ok(x), bad, u);
+  tally(c, bad, sdf::crm::sqrt_guard_g<0>(x), bad, u);
+}
+
+// the one-compare guard (SDF_CRM_SQRT_GUARD 1): every x but +INF
+__global__ void check_sqrt_bounded(unsigned base, Counts* c) {
+  const unsigned u = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const float x = __uint_as_float(u);
+  const float a = sdf::crm::cr_sqrt_g<1>(x), b = __builtin_sqrtf(x);
+  const bool bad = !same_bits(a, b);
+  tally(c, bad, sdf::crm::sqrt_guard_g<1>(x), bad && u != 0x7F800000u, u);
+}
+
+__global__ void check_sqrt_wide(unsigned base, Counts* c) {
+  const unsigned u = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const float x = __uint_as_float(u);
+  const bool in = (u - 0x00800000u) < (0x7F800000u - 0x00800000u);   // positive normal
+  const bool bad = in && !same_bits(sdf::crm::sqrt_fast(x), __builtin_sqrtf(x));
+  tally(c, bad, in, bad && u < 0x0D800000u, u);
 }
 
 __global__ void check_rcp(unsigned base, Counts* c) {
@@ -315,7 +339,9 @@ int main(int argc, char** argv) {
                 {"log", check_log, 1ull << 32, ""},   {"smin", check_smin, 1ull << 32, ""},
                 {"sminedge", check_smin_edges, 1ull << 32, ""},
                 {"pow", check_pow, kPowXEnd, ""}, {"minmax", check_minmax, 256, ""},
-                {"rcpneg", check_rcp_neg, 1ull << 32, ""}, {"div", check_div, 1ull << 32, ""}};
+                {"rcpneg", check_rcp_neg, 1ull << 32, ""}, {"div", check_div, 1ull << 32, ""},
+                {"sqrtwide", check_sqrt_wide, 1ull << 32, ""},
+                {"sqrtbounded", check_sqrt_bounded, 1ull << 32, ""}};
   // an argument selects checks by name (e.g. "sqrt,log"; "smin" matches only
   // itself)
   auto wanted = [&](const char* name) {

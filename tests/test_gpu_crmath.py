@@ -49,6 +49,25 @@ def test_cr_sqrt_is_ieee_sqrt_everywhere(results):
     assert r["fast_path"] == 200 * 2**23, r
 
 
+def test_cr_sqrt_one_compare_guard_is_ieee_on_every_finite_input(results):
+    """SDF_CRM_SQRT_GUARD 1 (the CSG units): guard x >= 2^-100 only; the one
+    input it gets wrong is +INF, which the working range keeps away."""
+    r = results["sqrtbounded"]
+    assert r["inputs"] == 2**32 and r["mismatch"] == 1 and r["effective"] == 0, r
+    assert r["first"] == [0x7F800000], r
+    # [2^-100, +INF]: 228 binades and +INF itself
+    assert r["fast_path"] == 228 * 2**23 + 1, r
+
+
+def test_sqrt_fast_path_exact_on_every_normal_from_2_pow_minus_100(results):
+    """The unguarded fast path on EVERY positive normal float: no mismatch
+    from 2^-100 up to FLT_MAX (what the one-compare guard admits); below
+    2^-100 ("effective") it fails, and both guards keep it out."""
+    r = results["sqrtwide"]
+    assert r["fast_path"] == 254 * 2**23, r
+    assert r["mismatch"] == r["effective"] > 0, r
+
+
 def test_rcp_fast_is_ieee_reciprocal_on_its_domain(results):
     r = results["rcp"]
     assert r["fast_path"] == 200 * 2**23 and r["mismatch"] == 0, r
