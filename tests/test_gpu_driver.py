@@ -135,7 +135,9 @@ def test_frame_not_shipped_is_refused(nccl_world1):
     # 16 buffer sets on the driver's 4 render streams, batches of
     # 8 shipped 8 frames late -- buffer sets share streams, and their waits
     # must not form a cycle across ranks
-    (3, "C3", None, 8, 16, False, 8), (2, "C5", None, 8, 16, True, 8)])
+    (3, "C3", None, 8, 16, False, 8), (2, "C5", None, 8, 16, True, 8),
+    # the Mandelbulb at world 8 (4K, default shares)
+    (8, "C5", None, 0, 0, False, 0)])
 def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, nonblocking, lag):
     """The native C++ driver's multi-rank sequence (render, RCCL-style length
     all-gather, send/recv of the TILES streams to rank 0, decode) with
