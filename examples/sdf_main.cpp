@@ -89,7 +89,7 @@ int run_driver(sdf::Frame f, int frames, const std::string& out) {
   // shares: SDF3D_SHARES="a:b", else what the cost model of bench.py picks
   // for this world size (sdf3d_amd/multigpu.py choose_shares)
   static const int kShares[9][2] = {{1, 1}, {1, 1}, {1, 1}, {1, 1}, {3, 4},
-                                    {3, 4}, {1, 2}, {1, 2}, {2, 7}};
+                                    {3, 4}, {1, 2}, {1, 2}, {1, 7}};
   int share_root = kShares[world < 9 ? world : 8][0], share_peer = kShares[world < 9 ? world : 8][1];
   if (std::sscanf(env("SDF3D_SHARES", "").c_str(), "%d:%d", &share_root, &share_peer) != 2) {
     share_root = kShares[world < 9 ? world : 8][0];

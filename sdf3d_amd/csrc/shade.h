@@ -47,15 +47,15 @@ enum TilesShade : uint32_t {
 // (tests/test_gpu_parity.py) checks it.  Where both ends of a 2^-44 interval around it round to the same
 // float, that float is the correct rounding of x^n -- and of the library's
 // fp64 pow, which lies in the same interval; other lanes (rounding
-// boundaries, NaN) take the library pow.  SDF_SHADE_LIBRARY_POW (the TILES
-// decoder, tiles.hip): the library pow alone -- the same floats; there its
-// code size keeps the decoder's tile loop rolled at 8 waves/SIMD, which
-// decodes fast-precision streams 2 % faster than the unrolled loop at 7.
+// boundaries, NaN) take the library pow.  SDF_SHADE_LIBRARY_POW 1: the
+// library pow alone -- the same floats (the TILES decoder used it until
+// round 5 to keep its tile loop rolled at 8 waves/SIMD; on exact-precision
+// streams it cost 0.084 ms of decode per 4K frame, tiles.hip).
 template <bool EXACT>
 __device__ __forceinline__ float spec_pow(float x, float shin) {
 #pragma clang fp contract(off)
   if constexpr (EXACT) {
-#ifndef SDF_SHADE_LIBRARY_POW
+#if !defined(SDF_SHADE_LIBRARY_POW) || !SDF_SHADE_LIBRARY_POW
     const int n = (int)shin;
     if ((float)n == shin && n >= 0 && n <= 64) {
       double b = (double)x, v = 1.0;

@@ -27,7 +27,12 @@
 #include <stdint.h>
 
 #include "kernel_args.h"
-#define SDF_SHADE_LIBRARY_POW 1   // see shade.h spec_pow
+// Exact-precision streams' specular term: 1 = the library fp64 pow alone
+// (through round 4), 0 = shade.h's repeated squaring with the library pow
+// only on lanes near a rounding boundary -- the same floats
+#ifndef SDF_SHADE_LIBRARY_POW
+#define SDF_SHADE_LIBRARY_POW 0
+#endif
 #include "shade.h"
 
 namespace sdf {

@@ -102,8 +102,14 @@ FRAME_COSTS_MS = {"render": 0.373, "render_tiles": 0.444, "decode": 0.043, "floo
 #   N = 2: 1:1 0.188, 4:3 0.204, 3:2 0.212
 #   N = 4: 3:4 0.102, 4:5 0.103, 2:3 0.105, 1:1 0.112
 #   N = 8: 2:7 0.0532, 1:4 0.0538, 1:3 0.0548
+# Round 5 at N = 8, rank 0's whole loop with rotated (non-resident) peer
+# streams and the busiest peer (tools/root_rccl_probe.py, root_probe.py;
+# profiles/r05_root_rccl_probe_*.json, r05_root_probe_exact_C4_*.json),
+# max(rank 0, peer) ms per frame: exact 1:7 0.0735, 1:4 0.0739, 2:7 0.0762;
+# fast rank 0 1:7 0.0564, 1:4 0.0612, 2:7 0.0630 -- and with RCCL's transfer
+# work on rank 0 too, 1:7 is the lightest (exact 0.126 against 0.137-0.140).
 # The cost model below serves the other world sizes (and explicit costs).
-MEASURED_SHARES = {2: (1, 1), 4: (3, 4), 8: (2, 7)}
+MEASURED_SHARES = {2: (1, 1), 4: (3, 4), 8: (1, 7)}
 
 
 def choose_shares(world: int, costs=None, max_blocks: int = 4) -> tuple[int, int]:

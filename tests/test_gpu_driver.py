@@ -148,7 +148,7 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, n
     place, and one FIFO engine per rank makes any cross-communicator order
     mismatch between ranks an error.  Rank 0's assembled last frame must equal a single-device
     render bit for bit; the 8-rank C4 case is the round-end N = 8 bench's
-    configuration (4K, default 2:7 shares, batches of 2 frames).  Frames
+    configuration (4K, default 1:7 shares, batches of 2 frames).  Frames
     are shipped in batches (1, 2, 4: one length all-gather and one send/recv
     group per batch; the warm-up's drain closes a short batch, so the next
     batch starts on a new buffer set).  `nonblocking`: the stand-in answers
@@ -187,7 +187,7 @@ def test_native_driver_multirank(tmp_path, nproc, cfg, shares, batch, streams, n
     assert d["config"]["wire"] == "tiles"
     assert d["config"]["batch"] == (batch or 2), d["config"]
     if nproc == 8:
-        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 2 / others 7")
+        assert d["config"]["tiling"].startswith("8-row blocks, rank 0 1 / others 7")
     import re
     counts = [int(m) for m in re.findall(r"shmcomm: inprogress_returns=(\d+)", r.stderr)]
     assert len(counts) >= nproc, r.stderr[-2000:]

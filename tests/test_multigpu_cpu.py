@@ -140,8 +140,9 @@ def test_choose_shares():
     assert a < b                            # rank 0 decodes 7 streams: fewer rows
     # with a free decode the shares balance renders alone
     assert choose_shares(8, {"render": 1.0, "render_tiles": 1.0, "decode": 0.0}) == (1, 1)
-    # the measured defaults (tools/root_probe.py, profiles/r03_share_probe_C4.json)
-    assert [choose_shares(w) for w in (2, 4, 8)] == [(1, 1), (3, 4), (2, 7)]
+    # the measured defaults (tools/root_probe.py, profiles/r03_share_probe_C4.json;
+    # N = 8 round 5: r05_root_rccl_probe_exact_C4.json)
+    assert [choose_shares(w) for w in (2, 4, 8)] == [(1, 1), (3, 4), (1, 7)]
     # every default tiling covers the frame exactly once
     for w in range(2, 9):
         a, b = choose_shares(w)
