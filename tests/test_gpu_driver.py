@@ -272,3 +272,27 @@ def test_native_driver_refuses_malformed_stream():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["error"] == abi.SDF_E_COMM, d
     assert d["frame1_exact"] and d["frame2_exact_outside"], d
+
+
+def test_reused_buffer_set_refuses_its_old_frame(nccl_world1):
+    """after a drain closes a short batch the next batch
+    starts on a new buffer set, so later frames reuse buffer sets out of
+    index order; a frame whose buffer set now holds a newer frame must be
+    refused (sdf_driver_frame's owner check), not handed out with another
+    frame's pixels.  nbuf 8, batches of 4: frames 0-1, drain, frames 2-7 land
+    in sets 4-7 and 0-1, so frame 0's set holds frame 6."""
+    from sdf3d_amd import abi, scenes
+    from sdf3d_amd.driver import NativeFrameDriver
+    f = scenes.config("C3", 96, 64, precision=abi.PRECISION_FAST)
+    drv = NativeFrameDriver(f, 0, 1, "cuda:0", nbuf=8, lag=2, dist=nccl_world1,
+                            root_as_peer=True, batch=4)
+    first = [drv.step() for _ in range(2)]
+    drv.drain()
+    later = [drv.step() for _ in range(6)]
+    drv.drain()
+    with pytest.raises(abi.SdfError):
+        drv.read_frame(first[0])         # its buffer set now holds a later frame
+    got = drv.read_frame(later[-1])
+    torch.cuda.synchronize()
+    drv.close()
+    assert torch.equal(got.view(torch.int32), _reference(f).view(torch.int32))
