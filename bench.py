@@ -31,7 +31,10 @@ vector peak, with the counter-based VALU busy of the same PMC run and, as
 tests/golden/stats_<cfg>_p0.npz) over the same time (see roofline()).
 `cpu_baseline` times the CPU oracle (a restatement of the reference shader:
 the reference's own OpenCL kernel is empty and no CPU OpenCL device exists)
-on whole frames of the same workload, rank 0 at N=1 only.
+on whole frames of the same workload, rank 0 at N=1 only; its last frame is
+then the checker of the frames just timed (`parity.same_run`, `frame_verified`
+at N=1: the last timed frame against it, pixel by pixel, after the timed
+region).
 """
 from __future__ import annotations
 
@@ -283,7 +286,9 @@ def cpu_baseline(frame, stride, frames):
     """The CPU oracle (the reference shader restated: its own OpenCL kernel
     is empty and no CPU OpenCL device exists) on whole frames (stride 1) or
     every stride-th 8-row block, OpenMP over the host threads this process
-    may use, median of `frames` after one warm-up."""
+    may use, median of `frames` after one warm-up.
+    Returns (the JSON object, the last oracle frame [rows, W, 4], the frame
+    rows it holds): the frame is the checker of same_run_parity()."""
     import oracle
     from sdf3d_amd import renderer as R
     t = R.tiling(0, stride, 8) if stride > 1 else None
@@ -293,10 +298,14 @@ def cpu_baseline(frame, stride, frames):
     times = []
     for _ in range(frames):
         t0 = time.perf_counter()
-        oracle.render(frame, t, nthreads=n, variant="baseline")
+        rgba, _ = oracle.render(frame, t, nthreads=n, variant="baseline")
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     px = rows * frame.params.width
+    H = frame.params.height
+    ys = (np.arange(H) if stride <= 1 else
+          np.array([y for y in range(H) if (y // 8) % stride == 0]))
+    assert len(ys) == rows
     what = ("whole frames" if stride <= 1 else
             f"every {stride}th 8-row block ({rows} rows, {px} px)")
     return {"value": round(px / med / 1e6, 4), "unit": "Mpixels/s", "cores": n, "kind": "port",
@@ -305,7 +314,30 @@ def cpu_baseline(frame, stride, frames):
                       f"median of {frames} after 1 warm-up, {n} OpenMP threads (the process's "
                       f"CPU affinity), CPU oracle (oracle/oracle_core.h, gcc -O3 "
                       f"-march=x86-64-v4 -ffp-contract=off, no fast-math)",
-            "seconds_per_sample": round(med, 3)}
+            "seconds_per_sample": round(med, 3)}, rgba, ys
+
+
+def same_run_parity(gpu_frame, ref, ys, precision):
+    """The last TIMED frame (rank 0's, read back after the run) against the
+    CPU oracle frame cpu_baseline() rendered of the same workload, on the
+    rows the oracle rendered: per pixel, its largest per-channel |GPU -
+    oracle|; an outlier exceeds north_star's 1e-4 (tests/parity.py's
+    policy, without the replay diagnosis)."""
+    g = gpu_frame.cpu().numpy()[ys]
+    bits = (g.view(np.uint32) == ref.view(np.uint32)).all(axis=-1)
+    err = np.abs(g.astype(np.float64) - ref.astype(np.float64)).max(axis=-1)
+    err = np.where(bits, 0.0, err)                      # equal bits, NaN included
+    nan = ~bits & np.isnan(err)
+    err = np.where(nan, np.inf, err)
+    out = int((err > 1e-4).sum())
+    return {"precision": precision, "pixels": int(bits.size), "bit_exact": int(bits.sum()),
+            "outliers_over_1e-4": out, "over_0.05": int((err > 0.05).sum()),
+            "max_err": float(err.max()) if err.size else 0.0,
+            "within_1e-4_everywhere": out == 0,
+            "rows": ("all" if len(ys) == gpu_frame.shape[0] else
+                     f"{len(ys)} rows (every block the CPU sample rendered)"),
+            "what": "last timed frame of this run vs the CPU oracle frame rendered for "
+                    "cpu_baseline (same scene, camera, size), compared after the timed region"}
 
 
 def main():
@@ -536,13 +568,13 @@ def main():
     # frame, tests/test_gpu_parity.py test_full_size_pixel_parity); the fast
     # precision (FMA contraction, hardware sqrt/rcp: within 1e-4 except at a
     # few branch flips, profiles/parity_fullsize.json) is this sub-object
-    other = None
+    other, drv_other = None, None
     other_name = "fast" if prec == abi.PRECISION_EXACT else "exact"
     if world == 1 and not args.no_exact:
         fe = frame.copy()
         fe.params.precision = (abi.PRECISION_FAST if prec == abi.PRECISION_EXACT
                                else abi.PRECISION_EXACT)
-        el_e, _, _ = timed_run(fe, args.steps, args.warmup)
+        el_e, _, drv_other = timed_run(fe, args.steps, args.warmup)
         fek = fe.copy()
         fek.params.output_format = abi.FORMAT_RGBA32F
         kavg_e = kernel_avg_ms(fek)
@@ -647,7 +679,24 @@ def main():
         out["parity"] = parity_summary(args.config, args.precision)
         if world == 1 and not args.no_cpu_baseline:
             log("[bench] cpu baseline ...")
-            out["cpu_baseline"] = cpu_baseline(frame, args.cpu_sample_stride, args.cpu_frames)
+            out["cpu_baseline"], ref, ys = cpu_baseline(frame, args.cpu_sample_stride,
+                                                        args.cpu_frames)
+            # parity as a fact of this run: the frames just timed against the
+            # oracle frame the baseline rendered (no extra timed work)
+            if native and args.format == "rgba32f":
+                got = drv.read_frame(k_steps - 1)
+                torch.cuda.synchronize(dev)
+                sr = same_run_parity(got, ref, ys, args.precision)
+                out["parity"]["same_run"] = sr
+                out["frame_verified"] = sr["within_1e-4_everywhere"]
+                out["frame_verified_what"] = ("N=1: the last timed frame within 1e-4 of the CPU "
+                                              "oracle on every compared pixel (parity.same_run)")
+                if other is not None and hasattr(drv_other, "read_frame"):
+                    got = drv_other.read_frame(k_steps - 1)
+                    torch.cuda.synchronize(dev)
+                    other["parity"]["same_run"] = same_run_parity(got, ref, ys, other_name)
+                log(f"[bench] same-run parity: {sr['bit_exact']}/{sr['pixels']} bit-exact, "
+                    f"{sr['outliers_over_1e-4']} over 1e-4, max err {sr['max_err']:.3g}")
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

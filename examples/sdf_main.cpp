@@ -173,7 +173,13 @@ int main(int argc, char** argv) {
       f.params.flags = SDF_FLAG_SHADOW | SDF_FLAG_AO;
       f.params.normal_mode = SDF_NORMAL_TETRA;
     }
-    f.params.precision = SDF_PRECISION_FAST;
+    // EXACT (the default): the oracle's fp32 operation sequence, every pixel
+    // bit-identical to it at 4K.  SDF3D_PRECISION=fast opts into FMA
+    // contraction and hardware sqrt/rcp: 1.47x faster on C4, but a few
+    // grazing pixels end their march a step apart (C4: 48 pixels over 1e-4,
+    // max 0.72; C5: 2,123, max 0.34; profiles/parity_fullsize.json)
+    f.params.precision =
+        env("SDF3D_PRECISION", "exact") == "fast" ? SDF_PRECISION_FAST : SDF_PRECISION_EXACT;
     if (std::getenv("WORLD_SIZE") || env("SDF3D_DRIVER", "0") == "1")
       return run_driver(f, frames, out);
 

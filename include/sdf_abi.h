@@ -56,13 +56,17 @@ typedef __hip_internal::int64_t int64_t;
 extern "C" {
 #endif
 
-#define SDF_ABI_VERSION 10  /* 7: sdf_comm_create timeout, sdf_render_multi;
+#define SDF_ABI_VERSION 11  /* 7: sdf_comm_create timeout, sdf_render_multi;
                                 8: sdf_render_frames;
                                 9: TILES carries shading terms (64-byte
                                    stream header), SDF_FORMAT_SHADE32F;
                                 10: sdf_driver_config.batch (frames per
                                    ship); TILES base bits pixel by pixel
-                                   (lane-major) instead of bit planes */
+                                   (lane-major) instead of bit planes;
+                                11: sdf_schedule_*, sdf_render_scheduled,
+                                   sdf_tiles_decode_checked (SDF_TILES_BAD_*
+                                   one byte each), sdf_validate bounds every
+                                   length to 1e15 */
 
 /* ---- status codes ------------------------------------------------------ */
 #define SDF_OK               0
@@ -442,9 +446,11 @@ int sdf_tiles_decode(const void* parts, int32_t nparts, int64_t part_stride,
  *           part r is malformed -- asynchronous, like the decode.  With
  *           status == NULL the call waits for the decode on `stream` and
  *           returns SDF_E_COMM when some part was malformed. */
-#define SDF_TILES_BAD_HEADER 1u
-#define SDF_TILES_BAD_TILE   2u
-#define SDF_TILES_BAD_FIELD  4u
+/* One byte per cause (ABI 11): each is set by a byte store of its own, so
+ * the causes of a part combine without atomics (waves of one part race). */
+#define SDF_TILES_BAD_HEADER 0x000001u
+#define SDF_TILES_BAD_TILE   0x000100u
+#define SDF_TILES_BAD_FIELD  0x010000u
 int sdf_tiles_decode_checked(const void* parts, int32_t nparts, int64_t part_stride,
                              const sdf_tiling* tilings, const int64_t* used, int32_t width,
                              int32_t height, void* frame, uint32_t* status, void* stream);

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-SDF_ABI_VERSION = 10
+SDF_ABI_VERSION = 11
 MAX_DECODE_PARTS = 64   # SDF_MAX_DECODE_PARTS
 SDF_MAX_PRIMS = 16
 
@@ -50,7 +50,7 @@ FORMAT_CHANNELS = {FORMAT_RGBA32F: 4, FORMAT_RGBA16F: 4, FORMAT_RGBA8: 4, FORMAT
                    FORMAT_SHADE32F: 4}
 TILES_HEADER_BYTES = 64   # used, ntiles, shade mode, 0, shading constants (sdf_abi.h)
 # sdf_tiles_decode_checked status bits (sdf_abi.h SDF_TILES_BAD_*)
-TILES_BAD_HEADER, TILES_BAD_TILE, TILES_BAD_FIELD = 1, 2, 4
+TILES_BAD_HEADER, TILES_BAD_TILE, TILES_BAD_FIELD = 0x1, 0x100, 0x10000
 
 
 class sdf_primitive(C.Structure):
@@ -200,15 +200,20 @@ def load_library(path: Path | str | None = None, any_version: bool = False) -> C
             f"{p} is missing: build the HIP library first (python -m sdf3d_amd.build). "
             "There is no CPU fallback on the product path.")
     lib = C.CDLL(str(p))
+    # the version first: a stale library lacks later entry points, and the
+    # mismatch is the message to give, not a missing symbol
+    lib.sdf_abi_version.restype = C.c_int
+    lib.sdf_abi_version.argtypes = []
+    v = lib.sdf_abi_version()
+    if v != SDF_ABI_VERSION and not any_version:
+        raise RuntimeError(f"libsdf3d ABI version {v} != {SDF_ABI_VERSION}: rebuild it "
+                           "(python -m sdf3d_amd.build)")
     for name, (res, args) in SIGNATURES.items():
         if any_version and not hasattr(lib, name):
             continue   # an older build without a later entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    v = lib.sdf_abi_version()
-    if v != SDF_ABI_VERSION and not any_version:
-        raise RuntimeError(f"libsdf3d ABI version {v} != {SDF_ABI_VERSION}")
     if path is None:
         _lib = lib
     return lib

@@ -224,13 +224,36 @@ __device__ __forceinline__ void div3(float& a0, float& a1, float& a2, float l) {
 }
 
 // n / k for the smooth-min (n in [0, k], any positive finite k), from the
-// host-prepared sc = 2^s with k sc in [2^-22, 2) (s <= 127) and ys =
+// host-prepared sc = 2^s with k sc in [2^-22, 1) (s <= 127) and ys =
 // RN(1/(k sc)): n/k = (n sc)/(k sc) exactly, k sc is exact, n sc is exact
 // unless it underflows (then h < 2^-104), and Markstein's conditions hold
-// for n sc >= 2^-100.  Below that h < 2^-78 on both paths, so h*h -- all the
+// for n sc >= 2^-100.  Below that h < 2^-77 on both paths, so h*h -- all the
 // smooth-min uses -- is +0 on both: the smooth-min's result is bit-identical.
 __device__ __forceinline__ float div_scaled(float n, float k, float sc, float ys) {
   return div_prepared(n * sc, k * sc, ys);
+}
+
+// The smooth-min's whole h = max(k - |e|, 0) / k (e = RN(a - b)) from the
+// same preparation, ksc = k sc (exact), in 4 instructions instead of 6
+// (round 6, tools/block_counts.py: the smooth-min was 12 VALU, ~400 per
+// wave on C4):
+//   n' = clamp(RN(ksc - |e| sc), 0, 1): ONE FMA whose product |e| sc is exact,
+//        with the clamp bit for the max (n' <= ksc < 1, so the clamp's upper
+//        end never binds; no operand is NaN in the working range);
+//   h  = div_prepared(n', ksc, ys).
+// Against div_scaled(max(RN(k - |e|), 0), k, sc, ys): RN((k - |e|) sc) =
+// RN(k - |e|) sc exactly whenever both lie in the normal range (scaling by a
+// power of two commutes with rounding there); a difference k - |e| below
+// 2^-126 is exact already (a difference of floats that small is
+// representable), so both round the same exact product; otherwise the scaled
+// value is below 2^-126 < 2^-100 on both paths, where h*h is +0 on both (see
+// div_scaled).  A non-positive k - |e| gives +0 on both (an exact zero sum is
+// +0 in round-to-nearest).  Checked on the GPU (tests/crmath "sminh":
+// sampled k over every positive float, |e| around k, tiny, huge).
+__device__ __forceinline__ float smin_h(float e, float sc, float ksc, float ys) {
+  const float n =
+      __builtin_amdgcn_fmed3f(__builtin_fmaf(-__builtin_fabsf(e), sc, ksc), 0.0f, 1.0f);
+  return div_prepared(n, ksc, ys);
 }
 
 // ---- natural log ----------------------------------------------------------

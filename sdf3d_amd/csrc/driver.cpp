@@ -209,6 +209,15 @@ bool debug_on() {
   }();
   return on;
 }
+// SDF3D_DRIVER_DEBUG=2: also hand out the frames of a driver that has failed
+// (fault diagnosis only: a malformed stream's tiles then hold older pixels)
+bool debug_read_failed() {
+  static const bool on = [] {
+    const char* e = std::getenv("SDF3D_DRIVER_DEBUG");
+    return e && std::atoi(e) >= 2;
+  }();
+  return on;
+}
 int hip_ok(hipError_t e, int line = __builtin_LINE()) {
   if (e == hipSuccess) return SDF_OK;
   if (debug_on())
@@ -822,6 +831,13 @@ static int driver_drain(sdf_driver* d) {
 int sdf_driver_frame(sdf_driver* d, int64_t index, void** rgba) {
   if (!d || !rgba) return SDF_E_INVALID_ARG;
   *rgba = nullptr;
+  // a driver that has failed hands out no frame: a malformed peer stream
+  // leaves its tiles holding an older frame's pixels; the
+  // status words of decodes already completed are polled here too
+  if (!debug_read_failed()) {
+    if (d->error != SDF_OK) return d->error;
+    if (check_streams(d) != SDF_OK) return d->error;
+  }
   if (!d->root || index < 0 || index >= d->next || index < d->next - d->nbuf)
     return SDF_E_INVALID_ARG;
   // with collectives a frame holds the peers' rows only once it has been

@@ -33,7 +33,8 @@ Schedule* schedule_create(int rows, int period);
 void schedule_destroy(Schedule* s);
 // before a launch: the latest order (once a cost snapshot has landed) into
 // plan->order, and the cost buffer the kernel adds to
-void schedule_apply(Schedule* s, RenderPlan* plan);
+// SDF_E_HIP when the last cost copy failed (the schedule then measures anew)
+int schedule_apply(Schedule* s, RenderPlan* plan);
 // after the launch on `stream`: every `period` launches a snapshot of the
 // costs is copied to the host, behind the launch
 int schedule_after(Schedule* s, void* stream);

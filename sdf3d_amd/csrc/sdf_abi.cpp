@@ -126,13 +126,14 @@ void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
     o.reserved = in.k > 0.0f ? 1.0f / in.k : 0.0f;
     o.p[11] = in.k * 0.25f;  // smooth-min k/4 (fast precision)
     // exact precision's smooth-min division n / k (render_kernel.inc smin,
-    // cr_math.h div_scaled): sc = 2^s with k sc in [1, 2) (s <= 127, so a
-    // denormal k lands in [2^-22, 2)), and RN(1/(k sc)) by an IEEE division
+    // cr_math.h smin_h / div_scaled): sc = 2^s with k sc in [0.5, 1) (s <=
+    // 127, so a denormal k lands in [2^-22, 1)), and RN(1/(k sc)) by an IEEE
+    // division.  k sc < 1: smin_h's clamp to [0, 1] is its max(., 0) alone
     float sc = 1.0f, ks = 1.0f;
     if (in.k > 0.0f && std::isfinite(in.k)) {
       int e = 0;
       (void)std::frexp(in.k, &e);                 // k = m 2^e, m in [0.5, 1)
-      sc = std::ldexp(1.0f, std::min(1 - e, 127));
+      sc = std::ldexp(1.0f, std::min(-e, 127));
       ks = in.k * sc;                             // exact
     }
     o.p[9] = sc;
@@ -524,11 +525,19 @@ void schedule_destroy(Schedule* s) {
   delete s;
 }
 
-void schedule_apply(Schedule* s, RenderPlan* plan) {
+int schedule_apply(Schedule* s, RenderPlan* plan) {
   plan->order.n = 0;
   plan->order.cost = nullptr;
-  if (!s || plan->rows != s->rows) return;   // another shape: launch order, no costs
-  if (s->pending && hipEventQuery(s->ev) == hipSuccess) {
+  if (!s || plan->rows != s->rows) return SDF_OK;   // another shape: launch order, no costs
+  const hipError_t q = s->pending ? hipEventQuery(s->ev) : hipErrorNotReady;
+  if (s->pending && q != hipSuccess && q != hipErrorNotReady) {
+    // the copy of the costs failed: stop waiting for it and
+    // report the error; the next call measures again
+    (void)hipGetLastError();
+    s->pending = false;
+    return SDF_E_HIP;
+  }
+  if (s->pending && q == hipSuccess) {
     s->pending = false;
     std::vector<std::pair<unsigned long long, int>> d(s->nblocks);
     unsigned long long total = 0;
@@ -553,6 +562,7 @@ void schedule_apply(Schedule* s, RenderPlan* plan) {
   plan->order.cost = s->measure ? s->cost : nullptr;
   plan->order.n = s->n;
   if (s->n) std::memcpy(plan->order.order, s->order.data(), sizeof(uint16_t) * s->n);
+  return SDF_OK;
 }
 
 int schedule_after(Schedule* s, void* stream) {
@@ -609,7 +619,10 @@ int sdf_render_scheduled(const sdf_scene* scene, const sdf_camera* camera, const
   int rc = sdf::make_render_plan(scene, camera, light, material, params, tiling, rgba, steps,
                                  &plan);
   if (rc != SDF_OK) return rc;
-  if (schedule) sdf::schedule_apply(schedule->s, &plan);
+  if (schedule) {
+    rc = sdf::schedule_apply(schedule->s, &plan);
+    if (rc != SDF_OK) return rc;
+  }
   rc = sdf::launch_render_plan(plan, stream);
   if (rc == SDF_OK && schedule && plan.rows == schedule->s->rows)
     rc = sdf::schedule_after(schedule->s, stream);
@@ -720,9 +733,14 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
   if (p.width <= 0 || p.height <= 0 || p.width > 65536 || p.height > 65536)
     return SDF_E_INVALID_ARG;
   if (p.max_steps < 0 || p.max_steps > (1 << 24)) return SDF_E_INVALID_ARG;
-  if (!std::isfinite(p.max_dist) || !std::isfinite(p.eps) || !std::isfinite(p.shadow_k) ||
-      !std::isfinite(p.normal_eps) || !std::isfinite(p.shadow_offset))
-    return SDF_E_INVALID_ARG;
+  // every length the marches add to a coordinate stays in the working range
+  // (kMaxCoord below): normal_eps^2 and the AO tap lengths must not overflow,
+  // which the exact kernels' one-compare cr_sqrt guard relies on
+  for (float v : {p.max_dist, p.eps, p.shadow_k, p.normal_eps, p.shadow_offset})
+    if (!(std::fabs(v) <= kMaxCoord)) return SDF_E_INVALID_ARG;
+  if (p.flags & SDF_FLAG_AO)
+    for (float v : {p.ao_step, p.ao_base, p.ao_falloff, p.ao_strength})
+      if (!(std::fabs(v) <= kMaxCoord)) return SDF_E_INVALID_ARG;
   if (p.flags & ~(SDF_FLAG_SHADOW | SDF_FLAG_AO)) return SDF_E_INVALID_ARG;
   if (p.normal_mode != SDF_NORMAL_CENTRAL && p.normal_mode != SDF_NORMAL_TETRA)
     return SDF_E_INVALID_ARG;
@@ -756,7 +774,13 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
       }
     }
   } else if (scene->kind == SDF_SCENE_MANDELBULB) {
-    if (!(scene->bulb_scale > 0.0f) || !finite3(scene->bulb_center)) return SDF_E_INVALID_ARG;
+    // local coordinates (p - c) * RN(1/scale) stay finite: |p - c| <= ~3e15
+    // and 1/scale <= 1e15, so the exact kernel's Markstein steps (unbounded
+    // above, BulbScene::local) never see an overflowing product
+    if (!(scene->bulb_scale >= 1.0f / kMaxCoord && scene->bulb_scale <= kMaxCoord))
+      return SDF_E_INVALID_ARG;
+    for (float v : scene->bulb_center)
+      if (!(std::fabs(v) <= kMaxCoord)) return SDF_E_INVALID_ARG;
     if (scene->bulb_iterations < 1 || scene->bulb_iterations > 64) return SDF_E_INVALID_ARG;
     // bailout in (0, 2^32]: its square stays finite, so every iteration's
     // x^2 + z^2 <= m <= bailout^2 is finite (the exact kernel's 1 / sqrt of it,

@@ -135,9 +135,12 @@ __device__ __forceinline__ void decode_body(const DecodeParts& D, const uint8_t*
   const uint4 hdv = lane < nt ? reinterpret_cast<const uint4*>(base + Lt.head)[tbase + lane]
                               : make_uint4(0u, 0u, 0u, 0u);
   const long long want = D.used[part];
-  // a malformed part is reported (lane 0's store: a vector store) and skipped
+  // a malformed part is reported and skipped: lane 0 stores 1 into the
+  // cause's own byte of the part's word (a vector byte store), so the causes
+  // found by different waves of one part combine without atomics
   auto report = [&](uint32_t code) {
-    if (D.status && lane == 0) D.status[part] = code;
+    if (D.status && lane == 0)
+      reinterpret_cast<uint8_t*>(D.status + part)[__builtin_ctz(code) >> 3] = 1;
   };
   if (present == 0) {   // no stream: rows rendered in place -- unless one was sent
     if (want >= 0) report(kTilesBadHeader);

@@ -19,6 +19,10 @@
 //          (ADVICE r03): denormal k; k within 2^20 ulps of FLT_MAX; k >= 2^64
 //          with n so small that n * sc underflows; tiny normal k (2^-126 ..
 //          2^-100)
+//   sminh / sminhedge : the smooth-min's whole h by smin_h (round 6: one
+//          clamped FMA + div_prepared) vs IEEE max(k - |e|, 0) / k, 2^32
+//          sampled (k, e) pairs each (k over every positive float / from the
+//          edge families; e of either sign, near k, tiny, denormal, huge)
 //   minmax : v_min_f32 / v_max_f32 vs the GLSL select on the operand pairs
 //          the exact kernel relies on (hw_min / hw_max)
 //   rcpneg : rcp_fast on the negative half of its domain
@@ -122,10 +126,10 @@ __global__ void check_smin(unsigned base, Counts* c) {
   const unsigned ki = i >> 12, ni = i & 4095u;
   const unsigned kbits = 1u + (unsigned)(((unsigned long long)hash32(ki) * 0x7F7FFFFFull) >> 32);
   const float k = __uint_as_float(kbits);
-  // the host's preparation (sdf_abi.cpp prepare_prims): sc = 2^min(1 - e, 127)
+  // the host's preparation (sdf_abi.cpp prepare_prims): sc = 2^min(-e, 127)
   // with k = m 2^e, m in [0.5, 1); ys = RN(1/(k sc))
   const int e = __builtin_amdgcn_frexp_expf(k);
-  const float sc = __builtin_ldexpf(1.0f, (1 - e) < 127 ? (1 - e) : 127);
+  const float sc = __builtin_ldexpf(1.0f, -e < 127 ? -e : 127);
   const float ys = 1.0f / (k * sc);
   float n;
   const unsigned h = hash32(i * 2654435761u + 12345u);
@@ -144,7 +148,7 @@ __global__ void check_smin(unsigned base, Counts* c) {
 // the smooth-min's host preparation and comparison (check_smin)
 __device__ __forceinline__ void smin_case(float k, float n, unsigned tag, Counts* c) {
   const int e = __builtin_amdgcn_frexp_expf(k);
-  const float sc = __builtin_ldexpf(1.0f, (1 - e) < 127 ? (1 - e) : 127);
+  const float sc = __builtin_ldexpf(1.0f, -e < 127 ? -e : 127);
   const float ys = 1.0f / (k * sc);
   if (!(n <= k)) n = k;
   const float a = sdf::crm::div_scaled(n, k, sc, ys), b = n / k;
@@ -178,6 +182,58 @@ __global__ void check_smin_edges(unsigned base, Counts* c) {
     n = __uint_as_float(kbits - (h & 0xFFFu) < kbits ? kbits - (h & 0xFFFu) : 0u);   // near k
   }
   smin_case(k, n, i, c);
+}
+
+// The smooth-min's whole h (cr_math.h smin_h, round 6: the subtraction from
+// k, the max and the scaling as one clamped FMA, then div_prepared) vs the
+// IEEE max(k - |e|, 0) / k the oracle computes, for e = RN(a - b) of either
+// sign: bits, and ("effective") h*h*k*0.25, what the smooth-min uses.  k as in
+// check_smin (every positive finite float, uniform in bits) or, with `edge`,
+// from check_smin_edges' families; |e| spread over [0, 2k] (most of it below
+// k), within 4096 ulps of k on both sides, tiny and denormal, and far above k.
+__device__ __forceinline__ void sminh_case(float k, float e, unsigned tag, Counts* c) {
+  const int ex = __builtin_amdgcn_frexp_expf(k);
+  const float sc = __builtin_ldexpf(1.0f, -ex < 127 ? -ex : 127);
+  const float ksc = k * sc;
+  const float ys = 1.0f / ksc;
+  const float a = sdf::crm::smin_h(e, sc, ksc, ys);
+  const float n = k - __builtin_fabsf(e);
+  const float b = (n > 0.0f ? n : 0.0f) / k;
+  const bool bad = !same_bits(a, b);
+  const bool eff = !same_bits(a * a * k * 0.25f, b * b * k * 0.25f);
+  tally(c, bad, true, eff, tag);
+}
+__device__ __forceinline__ float sminh_e(float k, unsigned kbits, unsigned ni, unsigned h) {
+  float e;
+  if (ni < 1536) e = k * 2.0f * (__uint_as_float(0x3F800000u | (h >> 9)) - 1.0f);   // [0, 2k)
+  else if (ni < 2560) e = __uint_as_float(h % kbits);                                // below k
+  else if (ni < 3072) e = __uint_as_float(h & 0x007FFFFFu);                          // denormal
+  else if (ni < 3840) {                                                              // near k
+    const unsigned d = h & 0xFFFu;
+    e = __uint_as_float((h & 0x1000u) ? (kbits + d < 0x7F800000u ? kbits + d : kbits)
+                                      : (kbits > d ? kbits - d : 0u));
+  } else e = __uint_as_float(kbits + (h % (0x7F7FFFFFu - kbits + 1u)));              // above k
+  return (h & 0x80000000u) ? -e : e;
+}
+__global__ void check_sminh(unsigned base, Counts* c) {
+  const unsigned i = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned ki = i >> 12, ni = i & 4095u;
+  const unsigned kbits = 1u + (unsigned)(((unsigned long long)hash32(ki * 31u + 7u) * 0x7F7FFFFFull) >> 32);
+  const unsigned h = hash32(i * 2654435761u + 99991u);
+  sminh_case(__uint_as_float(kbits), sminh_e(__uint_as_float(kbits), kbits, ni, h), i, c);
+}
+__global__ void check_sminh_edges(unsigned base, Counts* c) {
+  const unsigned i = base + blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned fam = i >> 30, ki = (i >> 12) & 0x3FFFFu, ni = i & 4095u;
+  const unsigned hk = hash32(ki * 0x9E3779B9u + fam + 17u), h = hash32(i * 2654435761u + 4242u);
+  unsigned kbits;
+  switch (fam) {
+    case 0: kbits = 1u + hk % 0x007FFFFEu; break;                    // denormal k
+    case 1: kbits = 0x7F7FFFFFu - (hk & 0xFFFFFu); break;            // near FLT_MAX
+    case 2: kbits = 0x3D800000u + hk % (0x3F800000u - 0x3D800000u); break;   // k in [2^-4, 1)
+    default: kbits = 0x00800000u + hk % (0x0D800000u - 0x00800000u); break;  // 2^-126..2^-100
+  }
+  sminh_case(__uint_as_float(kbits), sminh_e(__uint_as_float(kbits), kbits, ni, h), i, c);
 }
 
 // The hardware v_min_f32 / v_max_f32 against the GLSL select gmin/gmax on
@@ -338,6 +394,8 @@ int main(int argc, char** argv) {
   } checks[] = {{"rcp", check_rcp, 1ull << 32, ""},   {"sqrt", check_sqrt, 1ull << 32, ""},
                 {"log", check_log, 1ull << 32, ""},   {"smin", check_smin, 1ull << 32, ""},
                 {"sminedge", check_smin_edges, 1ull << 32, ""},
+                {"sminh", check_sminh, 1ull << 32, ""},
+                {"sminhedge", check_sminh_edges, 1ull << 32, ""},
                 {"pow", check_pow, kPowXEnd, ""}, {"minmax", check_minmax, 256, ""},
                 {"rcpneg", check_rcp_neg, 1ull << 32, ""}, {"div", check_div, 1ull << 32, ""},
                 {"sqrtwide", check_sqrt_wide, 1ull << 32, ""},

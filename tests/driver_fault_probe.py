@@ -37,6 +37,20 @@ def main():
         err, at = e.code, at or "step"
     rd = Renderer("cuda:0")
     ref, _ = rd.render(f)
+    if os.environ.get("SDF3D_DRIVER_DEBUG", "0") < "2":
+        # a failed driver refuses its frames (driver.cpp sdf_driver_frame)
+        try:
+            drv.read_frame(1)
+            read_error = 0
+        except abi.SdfError as e:
+            read_error = e.code
+        print(json.dumps({"error": err, "at": at, "steps": steps, "read_error": read_error}),
+              flush=True)
+        drv.handle and drv.lib.sdf_driver_destroy(drv.handle)
+        drv.handle = None
+        drv._close_comms()
+        dist.destroy_process_group()
+        return
     f1 = drv.read_frame(1)            # received intact
     f2 = drv.read_frame(2)            # its table entries 0..15 overwritten
     torch.cuda.synchronize()

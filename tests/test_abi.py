@@ -99,10 +99,41 @@ def test_validate_accepts_all_configs():
     lambda f: f.light.pos.__setitem__(2, 1e16),
     lambda f: setattr(f.params, "max_dist", 1e16),
     lambda f: [f.camera.view.__setitem__(i, 1e-16 if i % 5 == 0 else 0.0) for i in range(15)],
+    # every length the marches add stays in the working range
+    lambda f: setattr(f.params, "normal_eps", 1e20),
+    lambda f: setattr(f.params, "shadow_offset", -2e15),
+    lambda f: setattr(f.params, "eps", 1e16),
+    lambda f: setattr(f.params, "shadow_k", float("inf")),
 ])
 def test_validate_rejects(mutate):
     f = scenes.reference()
     mutate(f)
+    assert _validate(f) == abi.SDF_E_INVALID_ARG
+
+
+@pytest.mark.parametrize("field,value", [
+    ("ao_base", float("nan")), ("ao_step", 1e16), ("ao_falloff", float("inf")),
+    ("ao_strength", -1e20)])
+def test_validate_rejects_ao_outside_range(field, value):
+    f = scenes.config("C3")
+    assert _validate(f) == abi.SDF_OK
+    setattr(f.params, field, value)
+    assert _validate(f) == abi.SDF_E_INVALID_ARG
+    f.params.flags &= ~abi.FLAG_AO          # unused without AO
+    assert _validate(f) == abi.SDF_OK
+
+
+@pytest.mark.parametrize("center,scale", [
+    ((2e38, 0.0, 0.0), 0.5), ((0.0, -2e15, 0.0), 1.0), ((0.0, 0.0, 0.0), 1e-20),
+    ((0.0, 0.0, 0.0), 1e16), ((0.0, float("nan"), 0.0), 1.0)])
+def test_validate_rejects_bulb_outside_range(center, scale):
+    """The exact Mandelbulb's (p - c) * RN(1/scale) must stay finite (ADVICE
+    r05: its Markstein steps give NaN where IEEE division gives INF)."""
+    f = scenes.config("C5")
+    assert _validate(f) == abi.SDF_OK
+    for i, v in enumerate(center):
+        f.scene.bulb_center[i] = v
+    f.scene.bulb_scale = scale
     assert _validate(f) == abi.SDF_E_INVALID_ARG
 
 

@@ -8,8 +8,9 @@ cr_math.h), checked EXHAUSTIVELY on the GPU by tests/crmath/crmath_check.hip:
   * cr_log(x) is bit-identical to (float)log((double)x) -- the oracle's
     cr_logf (oracle/sdf_oracle.c), the Mandelbulb DE's log -- for all 2^32
     inputs;
-  * the smooth-min's h = n / k by div_scaled: its bits equal IEEE n / k, or
-    (only where h < 2^-78) h*h*k/4 does, over 2^32 SAMPLED (k, n) pairs with
+  * the smooth-min's h = n / k by div_scaled and (round 6) the whole
+    max(k - |e|, 0) / k by smin_h: its bits equal IEEE n / k, or (only where
+    h < 2^-77) h*h*k/4 does, over 2^32 SAMPLED (k, n) pairs with
     k log-uniform over every positive exponent and n over [0, k], and over
     2^32 more from its edge families (denormal k, k near FLT_MAX, n * sc
     underflowing, tiny normal k) -- its proof is Markstein's theorem;
@@ -32,7 +33,7 @@ EXE = Path(__file__).resolve().parent / "crmath" / "crmath_check"
 @pytest.fixture(scope="module")
 def results():
     assert EXE.exists(), "build() must produce tests/crmath/crmath_check"
-    r = subprocess.run([str(EXE)], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([str(EXE)], capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     out = Path("gpurun_out")
@@ -88,6 +89,15 @@ def test_smooth_min_division_is_bit_identical_where_it_counts(results):
 def test_smooth_min_division_edge_families(results):
     r = results["sminedge"]
     assert r["inputs"] == 2**32 and r["effective"] == 0, r
+
+
+def test_smooth_min_h_by_one_clamped_fma(results):
+    """cr_math.h smin_h (round 6): max(k - |e|, 0) / k with the subtraction,
+    the max and the scaling in one clamped FMA -- h*h*k/4 bit-identical to
+    the IEEE form on 2^32 sampled (k, e) pairs and 2^32 from edge families."""
+    for name in ("sminh", "sminhedge"):
+        r = results[name]
+        assert r["inputs"] == 2**32 and r["effective"] == 0, (name, r)
 
 
 def test_integer_pow_is_the_library_pow(results):

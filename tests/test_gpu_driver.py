@@ -241,7 +241,7 @@ def test_cpp_driver_multirank_arcball(tmp_path, world):
         assert p.returncode == 0, se[-2000:]
     assert f"rank 0 of {world}" in outs[0][0]
     img = _read_ppm(out)
-    f = scenes.config("C3", W, H, precision=abi.PRECISION_FAST)
+    f = scenes.config("C3", W, H, precision=abi.PRECISION_EXACT)   # sdf_main's default
     scenes.set_view(f, nav_views(frames)[-1])
     rd = Renderer("cuda:0")
     rgba, st = rd.render(f, steps=True)
@@ -263,8 +263,10 @@ def test_native_driver_refuses_malformed_stream():
     import sys
     from netutil import free_port
     from sdf3d_amd import abi
+    # SDF3D_DRIVER_DEBUG=2: the probe reads the failed driver's frames (a
+    # failed driver refuses them otherwise, test_failed_driver_refuses_frames)
     env = dict(os.environ, SHMCOMM_CORRUPT_RECV="3", SHMCOMM_TIMEOUT_MS="20000",
-               GPU_MAX_HW_QUEUES="8")
+               GPU_MAX_HW_QUEUES="8", SDF3D_DRIVER_DEBUG="2")
     r = subprocess.run([sys.executable, str(ROOT / "tests" / "driver_fault_probe.py"),
                         str(free_port())], capture_output=True, text=True, timeout=180,
                        cwd=ROOT, env=env)
@@ -272,6 +274,25 @@ def test_native_driver_refuses_malformed_stream():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["error"] == abi.SDF_E_COMM, d
     assert d["frame1_exact"] and d["frame2_exact_outside"], d
+
+
+def test_failed_driver_refuses_frames():
+    """once a malformed stream has failed the driver, its frames
+    are refused with the driver's error (the bad tiles hold older pixels)."""
+    import json
+    import subprocess
+    import sys
+    from netutil import free_port
+    from sdf3d_amd import abi
+    env = dict(os.environ, SHMCOMM_CORRUPT_RECV="3", SHMCOMM_TIMEOUT_MS="20000",
+               GPU_MAX_HW_QUEUES="8", SDF3D_DRIVER_DEBUG="0")
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "driver_fault_probe.py"),
+                        str(free_port())], capture_output=True, text=True, timeout=180,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["error"] == abi.SDF_E_COMM, d
+    assert d["read_error"] == abi.SDF_E_COMM, d
 
 
 def test_reused_buffer_set_refuses_its_old_frame(nccl_world1):

@@ -429,7 +429,7 @@ def test_cpp_host_program(renderer, tmp_path, scene_name, cfg):
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     img = read_ppm(out)
-    f = scenes.config(cfg, 160, 90, precision=abi.PRECISION_FAST)
+    f = scenes.config(cfg, 160, 90, precision=abi.PRECISION_EXACT)   # sdf_main's default
     scenes.set_view(f, scenes.orbit_view(180.0, 0.0))     # frame 1 of 2: yaw 180
     rgba, _ = gpu(renderer, f, steps=False)
     want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
@@ -668,7 +668,7 @@ def test_cpp_frame_driver(renderer, tmp_path, peer_root):
     assert r.returncode == 0, r.stderr
     assert "rank 0 of 1" in r.stdout
     img = read_ppm(out)
-    f = scenes.config("C3", 160, 90, precision=abi.PRECISION_FAST)
+    f = scenes.config("C3", 160, 90, precision=abi.PRECISION_EXACT)   # sdf_main's default
     scenes.set_view(f, scenes.orbit_view(180.0, 0.0))     # frame 1 of 2: yaw 180
     rgba, _ = gpu(renderer, f, steps=False)
     want = quantize(rgba, abi.FORMAT_RGBA8)[::-1, :, :3]
