@@ -138,6 +138,9 @@ void prepare_prims(const sdf_scene& s, sdf_primitive* out) {
     }
     o.p[9] = sc;
     o.p[10] = 1.0f / ks;
+    // the prepared block's k slot carries k sc for the exact kernel (its
+    // smooth-min reads k/4 from p[11] and k sc here; nothing else reads it)
+    o.k = ks;
     const float* q = in.p;
     float* p = o.p;
     switch (in.kind) {
@@ -763,10 +766,11 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
       if (pr.op < 0 || pr.op >= SDF_OP_COUNT) return SDF_E_INVALID_ARG;
       const bool smooth = pr.op == SDF_OP_SMOOTH_UNION || pr.op == SDF_OP_SMOOTH_SUBTRACT ||
                           pr.op == SDF_OP_SMOOTH_INTERSECT;
-      if (smooth && !(pr.k > 0.0f && std::isfinite(pr.k))) return SDF_E_INVALID_ARG;
+      // a smooth blend radius in [2^-64, 1e15]: the exact smooth-min's
+      // h h (k/4) relies on the lower end (render_kernel.inc smin)
+      if (smooth && !(pr.k >= 0x1p-64f && pr.k <= kMaxCoord)) return SDF_E_INVALID_ARG;
       for (float v : pr.p)
         if (!std::isfinite(v) || std::fabs(v) > kMaxCoord) return SDF_E_INVALID_ARG;
-      if (smooth && pr.k > kMaxCoord) return SDF_E_INVALID_ARG;
       if (pr.kind == SDF_PRIM_CAPSULE) {
         // a segment, not a point: h = dot(pa, ba) / dot(ba, ba) must be a number
         const float bax = pr.p[3] - pr.p[0], bay = pr.p[4] - pr.p[1], baz = pr.p[5] - pr.p[2];

@@ -22,7 +22,9 @@
 //   sminh / sminhedge : the smooth-min's whole h by smin_h (round 6: one
 //          clamped FMA + div_prepared) vs IEEE max(k - |e|, 0) / k, 2^32
 //          sampled (k, e) pairs each (k over every positive float / from the
-//          edge families; e of either sign, near k, tiny, denormal, huge)
+//          edge families; e of either sign, near k, tiny, denormal, huge);
+//          "effective" compares what the smooth-min subtracts: h h (k/4)
+//          (the kernel's form, k >= 2^-64) against ((h h) k) 0.25
 //   minmax : v_min_f32 / v_max_f32 vs the GLSL select on the operand pairs
 //          the exact kernel relies on (hw_min / hw_max)
 //   rcpneg : rcp_fast on the negative half of its domain
@@ -200,7 +202,10 @@ __device__ __forceinline__ void sminh_case(float k, float e, unsigned tag, Count
   const float n = k - __builtin_fabsf(e);
   const float b = (n > 0.0f ? n : 0.0f) / k;
   const bool bad = !same_bits(a, b);
-  const bool eff = !same_bits(a * a * k * 0.25f, b * b * k * 0.25f);
+  // what the kernel forms: h h (k/4) for the k sdf_validate admits (>= 2^-64),
+  // against the oracle's ((h h) k) 0.25; below, the unfolded product
+  const bool eff = k >= 0x1p-64f ? !same_bits(a * a * (k * 0.25f), b * b * k * 0.25f)
+                                 : !same_bits(a * a * k * 0.25f, b * b * k * 0.25f);
   tally(c, bad, true, eff, tag);
 }
 __device__ __forceinline__ float sminh_e(float k, unsigned kbits, unsigned ni, unsigned h) {

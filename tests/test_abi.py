@@ -104,6 +104,9 @@ def test_validate_accepts_all_configs():
     lambda f: setattr(f.params, "shadow_offset", -2e15),
     lambda f: setattr(f.params, "eps", 1e16),
     lambda f: setattr(f.params, "shadow_k", float("inf")),
+    # a smooth blend radius below 2^-64 (the exact smooth-min's h h (k/4))
+    lambda f: (setattr(f.scene.prims[1], "op", abi.OP_SMOOTH_UNION),
+               setattr(f.scene.prims[1], "k", 1e-20)),
 ])
 def test_validate_rejects(mutate):
     f = scenes.reference()
