@@ -430,6 +430,13 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
   a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
   a.bulb_iterations = scene->bulb_iterations;
   prepare_prims(*scene, a.prims);
+  // sd_capsule's Markstein division: every capsule's dot(ba, ba) (prepared
+  // p[7]) in [2^-30, 2^30)
+  a.capsule_div = 1;
+  for (int i = 0; i < a.prim_count; ++i)
+    if (a.prims[i].kind == SDF_PRIM_CAPSULE &&
+        !(a.prims[i].p[7] >= 0x1p-30f && a.prims[i].p[7] < 0x1p30f))
+      a.capsule_div = 0;
   if (scene->kind == SDF_SCENE_PRIMITIVES) prepare_bounds(*scene, a);
   a.bulb_inv_scale = 1.0f / scene->bulb_scale;
   a.rgba = rgba;
