@@ -63,9 +63,6 @@ struct KernelArgs {
   alignas(16) float bound[SDF_MAX_PRIMS][4];   // 16-B aligned: read as float4 vector loads
   alignas(16) float cluster[4];
   int32_t cluster_first;
-  // exact precision: every capsule's dot(ba, ba) lies in [2^-30, 2^30), so its
-  // h divides by Markstein steps (render_kernel.inc sd_capsule); 0: IEEE
-  int32_t capsule_div;
   // outputs
   void* rgba;           // rows * width pixels of `format`, packed rows
   int32_t* steps;       // rows * width int2 or null

@@ -430,13 +430,6 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
   a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
   a.bulb_iterations = scene->bulb_iterations;
   prepare_prims(*scene, a.prims);
-  // sd_capsule's Markstein division: every capsule's dot(ba, ba) (prepared
-  // p[7]) in [2^-30, 2^30)
-  a.capsule_div = 1;
-  for (int i = 0; i < a.prim_count; ++i)
-    if (a.prims[i].kind == SDF_PRIM_CAPSULE &&
-        !(a.prims[i].p[7] >= 0x1p-30f && a.prims[i].p[7] < 0x1p30f))
-      a.capsule_div = 0;
   if (scene->kind == SDF_SCENE_PRIMITIVES) prepare_bounds(*scene, a);
   a.bulb_inv_scale = 1.0f / scene->bulb_scale;
   a.rgba = rgba;
@@ -733,7 +726,8 @@ int sdf_owned_rows(int32_t height, const sdf_tiling* tiling) {
 // NaN, which the exact kernel's hardware minimum relies on (render_kernel.inc
 // smin<HW>).
 constexpr float kMaxCoord = 1e15f;
-constexpr float kMinCapsule2 = 1e-30f;
+constexpr float kMinCapsule2 = 0x1p-30f;
+constexpr float kMaxCapsule2 = 0x1p30f;
 
 int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_light* light,
                  const sdf_material* material, const sdf_params* params,
@@ -779,9 +773,13 @@ int sdf_validate(const sdf_scene* scene, const sdf_camera* camera, const sdf_lig
       for (float v : pr.p)
         if (!std::isfinite(v) || std::fabs(v) > kMaxCoord) return SDF_E_INVALID_ARG;
       if (pr.kind == SDF_PRIM_CAPSULE) {
-        // a segment, not a point: h = dot(pa, ba) / dot(ba, ba) must be a number
+        // a segment of length in [2^-15, 2^15): dot(ba, ba), computed as the
+        // kernels do, in [2^-30, 2^30) -- the exact kernel's Markstein
+        // division of h = dot(pa, ba) / dot(ba, ba) (render_kernel.inc
+        // sd_capsule) needs its divisor there
         const float bax = pr.p[3] - pr.p[0], bay = pr.p[4] - pr.p[1], baz = pr.p[5] - pr.p[2];
-        if (!(bax * bax + bay * bay + baz * baz >= kMinCapsule2)) return SDF_E_INVALID_ARG;
+        const float baba = bax * bax + bay * bay + baz * baz;
+        if (!(baba >= kMinCapsule2 && baba < kMaxCapsule2)) return SDF_E_INVALID_ARG;
       }
     }
   } else if (scene->kind == SDF_SCENE_MANDELBULB) {

@@ -306,6 +306,19 @@ def test_validate_rejects_degenerate_capsule():
     assert _validate(f) == abi.SDF_E_INVALID_ARG
 
 
+@pytest.mark.parametrize("length,ok", [(2.0**-15 * 1.01, True), (2.0**-15 * 0.99, False),
+                                       (2.0**15 * 0.99, True), (2.0**15 * 1.01, False)])
+def test_validate_capsule_length_range(length, ok):
+    """Round 6: capsule lengths in [2^-15, 2^15) -- dot(ba, ba) in [2^-30,
+    2^30), the exact kernel's Markstein division of h (render_kernel.inc
+    sd_capsule)."""
+    f = scenes.config("C3", 64, 64)
+    cap = [i for i in range(f.scene.count) if f.scene.prims[i].kind == abi.PRIM_CAPSULE][0]
+    pr = f.scene.prims[cap]
+    pr.p[3], pr.p[4], pr.p[5] = pr.p[0] + length, pr.p[1], pr.p[2]
+    assert _validate(f) == (abi.SDF_OK if ok else abi.SDF_E_INVALID_ARG)
+
+
 def test_schedule_and_checked_decode_refuse_bad_arguments():
     """Host-side argument checks of the round-5 entry points (no device)."""
     lib = abi.load_library()
