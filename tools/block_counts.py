@@ -82,6 +82,12 @@ def classify(op: str) -> str:
 def instrument(lines: list[str], kernel: str, frame_off: int, rgba_karg: int):
     """Insert the block counters into `kernel` of the assembly `lines`;
     returns (new lines, blocks: list of {id, label, ins: [(op, text, idx)]})."""
+    # spare VGPRs above the kernel's own (its .num_vgpr), 8 of them
+    global SPARE, NEXT_FREE
+    nv = next(int(m.group(1)) for l in lines
+              for m in [re.match(rf"\s*\.set {re.escape(kernel)}\.num_vgpr, (\d+)", l)] if m)
+    SPARE = (nv + 3) // 4 * 4
+    NEXT_FREE = SPARE + 8
     start = next(i for i, l in enumerate(lines) if re.match(rf"^{re.escape(kernel)}:", l))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
     body = lines[start + 1:end]
@@ -89,8 +95,10 @@ def instrument(lines: list[str], kernel: str, frame_off: int, rgba_karg: int):
         m = re.search(r"lgkmcnt\((\d+)\)", l)
         if m and int(m.group(1)) != 0:
             raise SystemExit(f"kernel waits on lgkmcnt({m.group(1)}): counters would disturb it")
-        if re.search(r"\bv(6[4-9]|7[01])\b|v\[(6[4-9]|7[01])", l):
-            raise SystemExit("kernel uses the spare VGPRs")
+        for m in re.finditer(r"\bv(\d+)\b|v\[(\d+):(\d+)\]", l):
+            hi = int(m.group(1) or m.group(3))
+            if hi >= SPARE:
+                raise SystemExit(f"kernel uses v{hi}, above its .num_vgpr {nv}")
     blocks, out = [], []
     state = {"open": False}
 
@@ -394,7 +402,12 @@ def stage(stack) -> str:
     return "entry / scene setup"
 
 
-KEYS = [("sqrt_fast", "cr_sqrt"), ("sqrt_guard", "cr_sqrt"), ("cr_sqrt", "cr_sqrt"),
+KEYS = [("log_fast", "cr_log"), ("log_round_ok", "cr_log"), ("cr_log", "cr_log"),
+        ("bulb_roots", "bulb: map"), ("bulb_map", "bulb: map"), ("bulb_step", "bulb: map"),
+        ("bulb_de", "bulb: DE"), ("de_div", "bulb: DE"), ("mandelbulb", "bulb: orbit loop"),
+        ("div3_prepared", "bulb: (p - c) / scale"), ("BulbScene::local", "bulb: (p - c) / scale"),
+        ("BulbScene::eval", "bulb: eval"),
+        ("sqrt_fast", "cr_sqrt"), ("sqrt_guard", "cr_sqrt"), ("cr_sqrt", "cr_sqrt"),
         ("rcp_fast", "rcp_fast"), ("div_refined", "Markstein division"),
         ("div3", "Markstein division"), ("div_scaled", "smin: h = n / k"),
         ("div_prepared", "smin: h = n / k"), ("smin", "smin"), ("spec_pow", "spec pow"),
@@ -520,21 +533,27 @@ def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
     b = sub.add_parser("build")
+    b.add_argument("--tag", default="blocks", help="variant directory under tools/_variants")
     b.add_argument("--unit", default="render_exact.hip")
     b.add_argument("--kernel", default=KERNEL_C4)
     b.add_argument("--frame-bytes", type=int, default=3840 * 2160 * 16)
     r = sub.add_parser("run")
+    r.add_argument("--tag", default="blocks", help="variant directory under tools/_variants")
     r.add_argument("--config", default="C4")
     r.add_argument("--precision", default="exact")
     r.add_argument("--pose", type=int, default=0)
     r.add_argument("--launches", type=int, default=1)
     r.add_argument("--out", default=None)
-    sub.add_parser("symbolize")
+    sy = sub.add_parser("symbolize")
+    sy.add_argument("--tag", default="blocks")
     p = sub.add_parser("report")
+    p.add_argument("--tag", default="blocks", help="variant directory under tools/_variants")
     p.add_argument("result")
     p.add_argument("--top", type=int, default=40)
     p.add_argument("--json", default=None)
     a = ap.parse_args()
+    global OUT
+    OUT = ROOT / "tools" / "_variants" / a.tag
     {"build": cmd_build, "run": cmd_run, "report": cmd_report,
      "symbolize": cmd_symbolize}[a.cmd](a)
 

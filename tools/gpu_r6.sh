@@ -17,6 +17,10 @@ for s in $STEPS; do
       timeout -k 10 300 python tools/block_counts.py run --config ${BCFG:-C4} --precision exact > gpurun_out/blocks_run.log 2>&1
       rc=$?; echo "blocks rc=$rc"; tail -1 gpurun_out/blocks_run.log
       fatal $rc && exit $rc ;;
+    blocks5)
+      timeout -k 10 300 python tools/block_counts.py run --tag blocks_bulb --config C5 --precision exact > gpurun_out/blocks5_run.log 2>&1
+      rc=$?; echo "blocks5 rc=$rc"; tail -1 gpurun_out/blocks5_run.log
+      fatal $rc && exit $rc ;;
     bench)
       timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.log
       rc=$?; echo "bench rc=$rc"; python -c "
