@@ -632,9 +632,12 @@ int sdf_driver_create(const sdf_scene* scene, const sdf_camera* camera, const sd
     return rc == SDF_OK ? (rc = hip_ok(hipMalloc(p, n ? n : 16))) : rc;
   };
   // render streams: one per buffer set, at most kRenderStreams distinct
-  // (buffer set b on stream b mod kRenderStreams): with the two
-  // communication streams they fit HIP's hardware queues (bench.py: 8)
-  constexpr int kRenderStreams = 4;
+  // (buffer set b on stream b mod kRenderStreams).  Round 6: up to 8 (was
+  // 4): a peer's share of the Mandelbulb frame, whose long tiles leave long
+  // launch tails, renders as TILES 11 % faster on 8 streams than on 4
+  // (tools/tiles_overhead_probe.py, profiles/r06_tiles_overhead.jsonl);
+  // bench.py keeps 4 buffer sets by default
+  constexpr int kRenderStreams = 8;
   d->streams.assign(std::min(c.nbuf, kRenderStreams), nullptr);
   for (hipStream_t& st : d->streams)
     if (rc == SDF_OK) rc = hip_ok(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));

@@ -241,7 +241,7 @@ static double cluster_sphere(const double (*c)[3], const double* r, int n, doubl
 // Bounding spheres and the cluster bound read by the fixed-scene kernels'
 // culling (kernel_args.h "exact bounding-volume culling").  Radii are computed
 // in double and rounded up.
-void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
+void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a, bool exact = false) {
   std::memset(a.bound, 0, sizeof(a.bound));
   a.cluster_first = s.count;
   double cen[SDF_MAX_PRIMS][3], rad[SDF_MAX_PRIMS];
@@ -283,6 +283,12 @@ void prepare_bounds(const sdf_scene& s, sdf::KernelArgs& a) {
     rad[i] = R;
     // K' = (k + R + margin) / (1 - kCullRel), rounded up (render_kernel.inc wave_near)
     a.bound[i][3] = float((k + R + sdf::kCullAbs) / (1.0 - sdf::kCullRel) * (1.0 + 1e-6));
+    // exact kernel (the prepared block's `reserved`, unused there): the
+    // offset of the gap an evaluated primitive's own value leaves in the
+    // culling cache, k + margin + 1e-4 R (render_kernel.inc step_cached,
+    // SDF_CULL_SGAP), rounded up
+    if (exact && sdf::cullable(kind, pr.op))
+      a.prims[i].reserved = float((k + sdf::kCullAbs + 1e-4 * R) * (1.0 + 1e-6));
   }
   int first = s.count;
   while (first > 0 && cull[first - 1]) --first;
@@ -430,7 +436,8 @@ int make_render_plan(const sdf_scene* scene, const sdf_camera* camera, const sdf
   a.bulb_bail2 = scene->bulb_bailout * scene->bulb_bailout;
   a.bulb_iterations = scene->bulb_iterations;
   prepare_prims(*scene, a.prims);
-  if (scene->kind == SDF_SCENE_PRIMITIVES) prepare_bounds(*scene, a);
+  if (scene->kind == SDF_SCENE_PRIMITIVES)
+    prepare_bounds(*scene, a, params->precision == SDF_PRECISION_EXACT);
   a.bulb_inv_scale = 1.0f / scene->bulb_scale;
   a.rgba = rgba;
   a.steps = steps;

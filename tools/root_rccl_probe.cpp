@@ -40,6 +40,22 @@
 
 namespace {
 
+// recvcopy's receive: ONE kernel per batch moves every stream of it (as an
+// RCCL group of receives is one kernel), 16 bytes per lane, grid-stride
+struct CopyList {
+  const uint4* src[32];
+  uint4* dst[32];
+  unsigned long long n16[32];   // 16-byte units (streams rounded up: parts are 256-B pitched)
+  int count;
+};
+__global__ void copy_streams(CopyList L) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (int j = 0; j < L.count; ++j)
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+         i < L.n16[j]; i += stride)
+      L.dst[j][i] = L.src[j][i];
+}
+
 struct Api {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*);
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
@@ -80,11 +96,19 @@ int main(int argc, char** argv) {
   // what runs per frame: full (render + RCCL + decode), norccl (the decode
   // reads the set's streams where they were rendered: no transfer), rccl
   // (the transfers only), decode (the decode only, from the rotated sets),
-  // render (rank 0's rows only)
+  // render (rank 0's rows only), recvcopy (round 6, VERDICT r05 #3: the
+  // RECEIVING side only -- render + decode, with the N - 1 streams of every
+  // frame arriving in fresh receive buffers by hipMemcpyAsync on the data
+  // stream, one device-to-device copy per stream, as rank 0's memory sees
+  // the peers' writes over xGMI; no RCCL send on this GPU), recvkernel (the
+  // same bytes moved by ONE copy kernel per batch, as an RCCL group of
+  // receives is one kernel)
   const std::string mode = argc > 7 ? argv[7] : "full";
-  const bool do_render = mode == "full" || mode == "norccl" || mode == "render";
+  const bool do_copy = mode == "recvcopy" || mode == "recvkernel";
+  const bool one_kernel = mode == "recvkernel";
+  const bool do_render = mode == "full" || mode == "norccl" || mode == "render" || do_copy;
   const bool do_rccl = mode == "full" || mode == "rccl";
-  const bool do_decode = mode == "full" || mode == "norccl" || mode == "decode";
+  const bool do_decode = mode == "full" || mode == "norccl" || mode == "decode" || do_copy;
   if (K <= 0 || WARM < 0 || B < 1 || NB < B || NB % B) die("arguments", -1);
   // ---- the frame description ----
   sdf_scene scene;
@@ -238,13 +262,34 @@ int main(int argc, char** argv) {
         nccl(R.GroupEnd(), "group end");
         hip(hipEventRecord(ev_recv[b0], ds), "event");
         }
+        if (do_copy) {
+          for (int f = 0; f < B; ++f) hip(hipStreamWaitEvent(ds, ev_dec[b0 + f], 0), "wait");
+          CopyList L{};
+          for (int f = 0; f < B; ++f) {
+            const int sf = (int)((i - B + 1 + f) % NS);
+            for (int r = 1; r < N; ++r) {
+              char* dst = static_cast<char*>(gathered[b0 + f]) + (size_t)r * pitch;
+              const size_t n = (size_t)(data_off[r] + used[sf][r]);
+              if (one_kernel && L.count < 32) {
+                L.src[L.count] = static_cast<const uint4*>(part[sf][r]);
+                L.dst[L.count] = reinterpret_cast<uint4*>(dst);
+                L.n16[L.count++] = (n + 15) / 16;
+              } else {
+                hip(hipMemcpyAsync(dst, part[sf][r], n, hipMemcpyDeviceToDevice, ds), "copy-in");
+              }
+            }
+          }
+          if (one_kernel) hipLaunchKernelGGL(copy_streams, dim3(512), dim3(256), 0, ds, L);
+          hip(hipEventRecord(ev_recv[b0], ds), "event");
+        }
         h_rccl += since(tc);
         const auto td = Clock::now();
         for (int f = 0; f < B && do_decode; ++f) {
           const int bf = b0 + f, sf = (int)((i - B + 1 + f) % NS);
           hipStream_t sb = rs[bf % NR];
-          if (do_rccl) hip(hipStreamWaitEvent(sb, ev_recv[b0], 0), "wait");
-          ok(sdf_tiles_decode_checked(do_rccl ? gathered[bf] : setbuf[sf], N, pitch, til.data(),
+          if (do_rccl || do_copy) hip(hipStreamWaitEvent(sb, ev_recv[b0], 0), "wait");
+          ok(sdf_tiles_decode_checked(do_rccl || do_copy ? gathered[bf] : setbuf[sf], N, pitch,
+                                      til.data(),
                                       used[sf].data(), W, H, frame[bf],
                                       status + (size_t)N * bf, sb),
              "decode");
@@ -276,7 +321,7 @@ int main(int argc, char** argv) {
   std::vector<unsigned char> a(frame_bytes), c(frame_bytes);
   hip(hipMemcpy(a.data(), frame[bl], frame_bytes, hipMemcpyDeviceToHost), "copy");
   hip(hipMemcpy(c.data(), ref, frame_bytes, hipMemcpyDeviceToHost), "copy");
-  const bool exact = mode != "full" && mode != "norccl"
+  const bool exact = mode != "full" && mode != "norccl" && !do_copy
                          ? true   // no whole frame is assembled
                          : std::memcmp(a.data(), c.data(), frame_bytes) == 0;
   std::printf("{\"mode\": \"%s\", \"world\": %d, \"shares\": \"%d:%d\", \"batch\": %d, \"nbuf\": %d, \"sets\": %d, "
