@@ -260,10 +260,23 @@ __device__ __forceinline__ float smin_h(float e, float sc, float ksc, float ys) 
 // log(2) as a double (the rounding error, 2^-54 relative, times |e| <= 126
 // stays far below the fast path's error bound)
 #define SDF_CRM_LN2 0.693147180559945309417232121458
-// relative error bound of log_fast's double result (analysis: series
-// truncation s^9/19 <= 2^-50 relative at |f| <= 0.1716, the refined
-// reciprocal and the ~20 fp64 roundings each <= 2^-52; a generous 2^-47)
+// relative error bound of log_fast's double result.  Round 6
+// (SDF_CRM_LOG_SHORT 1): the series to s^7/15 and ONE Newton step for the
+// reciprocal -- truncation s^8/17 <= 2^-44.8 relative at |f| <= 0.1716, the
+// reciprocal 2^-46 (v_rcp_f64's 2^-23, squared), ~17 fp64 roundings each
+// <= 2^-52: a generous 2^-42 (a lane whose value lies that close to a float
+// rounding boundary, ~2^-17 of them, takes the library log; the exhaustive
+// check of all 2^32 inputs is the proof that the bound holds); three fp64 operations fewer per log
+// (tools/block_counts.py: cr_log was 9 % of C5 exact's VALU issue).  0: the
+// round-5 evaluation (s^8/17, two Newton steps, 2^-47)
+#ifndef SDF_CRM_LOG_SHORT
+#define SDF_CRM_LOG_SHORT 1
+#endif
+#if SDF_CRM_LOG_SHORT
+#define SDF_CRM_LOG_EPS 2.2737367544323206e-13
+#else
 #define SDF_CRM_LOG_EPS 7.105427357601002e-15
+#endif
 
 // p s + c as a three-address v_fma_f64 with the coefficient c in an SGPR
 // pair (SDF_CRM_FMA64 1).  With the builtin the compiler keeps the Horner
@@ -296,11 +309,17 @@ __device__ __forceinline__ double log_fast(float x) {
   const double d = m + 1.0;                              // exact
   double y = __builtin_amdgcn_rcp(d);                    // ~2^-23 relative
   y = __builtin_fma(__builtin_fma(-d, y, 1.0), y, y);    // ~2^-46
+#if !SDF_CRM_LOG_SHORT
   y = __builtin_fma(__builtin_fma(-d, y, 1.0), y, y);    // ~2^-52
+#endif
   const double f = (m - 1.0) * y;                        // m - 1 exact
   const double s = f * f;
+#if SDF_CRM_LOG_SHORT
+  double p = 1.0 / 15.0;
+#else
   double p = 1.0 / 17.0;
   p = fma64(p, s, 1.0 / 15.0);
+#endif
   p = fma64(p, s, 1.0 / 13.0);
   p = fma64(p, s, 1.0 / 11.0);
   p = fma64(p, s, 1.0 / 9.0);
