@@ -6,8 +6,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for spec in ${SPECS:-C4:exact C4:fast}; do
-  IFS=: read -r c p <<< "$spec"
-  timeout -k 10 400 python tools/pmc_traffic.py --config $c --precision $p --out gpurun_out/pmc \
+  IFS=: read -r c p x <<< "$spec"
+  # a third field "f64" adds the fp64 VALU pass
+  timeout -k 10 600 python tools/pmc_traffic.py --config $c --precision $p --out gpurun_out/pmc \
+    ${x:+--$x} \
     > gpurun_out/pmc_${c}_$p.log 2>&1
   rc=$?; echo "pmc $c $p rc=$rc"
   [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc_${c}_$p.log; exit $rc; }

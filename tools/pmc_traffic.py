@@ -48,11 +48,16 @@ PASSES = [
     ["SQ_LEVEL_WAVES", "SQ_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_INSTS_VSKIPPED",
      "SQ_ACTIVE_INST_VMEM", "SQ_INST_LEVEL_SMEM"],
 ]
+# --f64: the fp64 VALU mix (C5's exact bulb runs its map in f64)
+F64_PASS = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+            "SQ_INSTS_VALU_TRANS_F64"]
 
 
 def run_pass(counters, cfg, prec, outdir, steps):
     d = outdir / ("pmc_" + "_".join(c.lower() for c in counters)[:60])
-    cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run",
+    # each pass under its own kill timer (a counter request the hardware
+    # cannot serve makes rocprofv3 hang)
+    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run",
            "--", sys.executable, str(ROOT / "bench.py"), "--config", cfg, "--precision", prec,
            "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-display", "--no-exact",
            "--streams", "1"]
@@ -79,11 +84,12 @@ def main():
     ap.add_argument("--precision", default="fast")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--out", default="gpurun_out/pmc")
+    ap.add_argument("--f64", action="store_true", help="add the fp64 VALU pass")
     args = ap.parse_args()
     outdir = ROOT / args.out
     outdir.mkdir(parents=True, exist_ok=True)
     res, errors = {}, {}
-    for counters in PASSES:
+    for counters in PASSES + ([F64_PASS] if args.f64 else []):
         v, err = run_pass(counters, args.config, args.precision, outdir, args.steps)
         if v is None:
             errors[",".join(counters)] = err
@@ -131,6 +137,9 @@ def main():
                                     "transcendental": trans / res["SQ_WAVES"],
                                     "other": other / res["SQ_WAVES"],
                                     "total": res["SQ_INSTS_VALU"] / res["SQ_WAVES"]}
+    f64 = [k for k in F64_PASS if k in res]
+    if f64 and "SQ_WAVES" in res:
+        out["valu_f64_per_wave"] = {k[len("SQ_INSTS_VALU_"):]: res[k] / res["SQ_WAVES"] for k in f64}
     calib = ROOT / "profiles" / "r02_valu_busy_calib.json"
     if res.get("SQ_ACTIVE_INST_VALU") and res.get("GRBM_GUI_ACTIVE") and calib.exists():
         # counter-based VALU busy, gfx950 normalisation calibrated on pure
