@@ -11,7 +11,7 @@
 //                           scaling + 2-candidate residual test + class
 //                           fix-up (17 instructions).
 //   div_prepared(a,b,yb) == a / b, given yb = RN(1/b) prepared on the host,
-//                           by Markstein's theorem (q within 1 ulp, r exact,
+//                           by one Markstein step (proof at div_refined:
 //                           fma(r, yb, q) = RN(a/b)) wherever a/b, q and r
 //                           neither overflow nor underflow (3 instructions
 //                           instead of 11).  div_scaled applies it to the
@@ -35,7 +35,7 @@
 // div_scaled's domain, the (k, n) pairs of the smooth-min, has ~2^64 points:
 // it is SAMPLED (2^32 pairs, k log-uniform over every positive float, plus
 // denormal k, k near FLT_MAX and n whose scaled value underflows); its
-// bit-identity rests on Markstein's theorem, not on the sample.
+// bit-identity rests on the one-step proof at div_refined, not on the sample.
 #pragma once
 
 #ifndef __HIPCC_RTC__
@@ -129,27 +129,51 @@ __device__ __forceinline__ float rcp_fast(float x) {
   return __builtin_fmaf(e, y, y);
 }
 
-// a / b = RN(a/b) from yb = RN(1/b) (Markstein): valid where no intermediate
-// underflows or overflows -- the caller's domain argument.
+// a / b = RN(a/b) from yb = RN(1/b) (one Markstein step, proven below at
+// div_refined): valid where no intermediate underflows or overflows -- the
+// caller's domain argument.
 __device__ __forceinline__ float div_prepared(float a, float b, float yb) {
   const float q = a * yb;
   const float r = __builtin_fmaf(-b, q, a);
   return __builtin_fmaf(r, yb, q);
 }
 
-// (a0, a1, a2) / l with ONE reciprocal (normalize's three divisions): from y
-// = RN(1/l) (rcp_fast), q = RN(a y) is within 1.5 ulp of a/l; one Markstein
-// step (residual l q - a exact by FMA) makes it faithful, a second one
-// correctly rounded (Markstein's theorem needs q within 1 ulp, so one step
-// alone is no proof).  The residual's sign convention keeps a signed zero
-// numerator's sign.  Domain: l in [2^-30, 2^30), every a zero or |a| >=
-// 2^-60 (quotients and residuals stay normal); other lanes of the wave take
-// the IEEE division.
+// a / l from y = RN(1/l) (the host's, or rcp_fast) by ONE Markstein step:
+// q0 = RN(a y), r = RN(l q0 - a), q1 = RN(q0 - r y) == RN(a/l) wherever
+// nothing underflows or overflows.  Proof (round 6; rounds 1-5 took a second
+// step because q0 need not be faithful):
+//   Let Q = a/l = mu 2^j (mu in [1,2)), u = ulp(Q), l = ml 2^e (ml in [1,2);
+//   a power-of-two l makes everything exact).  |y - 1/l| <= ulp(1/l)/2 gives
+//   |a y - Q| <= E u with E = mu (ml/2) / 2 < ml/2.
+//   * q0 faithful: Markstein's theorem (y within 1/2 ulp of 1/l, q0 within
+//     1 ulp of Q; r is then exact) gives q1 = RN(Q).
+//   * q0 not faithful: rounding past the float adjacent to Q needs |a y - Q|
+//     > u/2 + (distance from Q to that float), so Q lies within (E - 1/2) u
+//     of a float and at least (1 - E) u from every rounding midpoint.  With
+//     r = (l q0 - a)(1 + rho), |rho| <= 2^-24, and l y = 1 + delta, |delta| <
+//     2^-24, q0 - r y = Q + (Q - q0)(1 - (1 + delta)(1 + rho)) = Q + eps,
+//     |Q - q0| < 2u, |eps| < 2^-22 u (1 + 2^-24).  So q1 = RN(Q + eps) = RN(Q)
+//     unless (1 - E) u <= |eps|, i.e. E > 1 - 2^-22 (1 + 2^-24): impossible
+//     for ml <= 2 - 2^-20 (E < ml/2 <= 1 - 2^-21), i.e. for every divisor
+//     mantissa field <= 2^23 - 8.
+//   * the 8 largest mantissa fields (with a margin: the 64 largest) against
+//     every numerator mantissa, two binades: checked exhaustively
+//     (tests/crmath/markstein_window.c, tests/test_crmath_host.py) -- none
+//     differs from a / l.
+// The residual's sign convention keeps a signed zero numerator's sign (q0 =
+// +-0, r = +0, q1 = -0 + q0 = q0).  Domain: l in [2^-30, 2^30), every a zero
+// or |a| >= 2^-60 (quotients and residuals stay normal); other lanes of the
+// wave take the IEEE division.
+// SDF_CRM_DIV_STEPS 2: rounds 1-5's second step (A/B only; same results)
+#ifndef SDF_CRM_DIV_STEPS
+#define SDF_CRM_DIV_STEPS 1
+#endif
 __device__ __forceinline__ float div_refined(float a, float l, float y) {
   float q = a * y;
-  float r = __builtin_fmaf(l, q, -a);
-  q = __builtin_fmaf(-r, y, q);
-  r = __builtin_fmaf(l, q, -a);
+#if SDF_CRM_DIV_STEPS == 2
+  q = __builtin_fmaf(-__builtin_fmaf(l, q, -a), y, q);
+#endif
+  const float r = __builtin_fmaf(l, q, -a);
   return __builtin_fmaf(-r, y, q);
 }
 // the divisor's magnitude in [2^-30, 2^30) (either sign)
@@ -192,7 +216,7 @@ __device__ __forceinline__ void div3_prepared(float& a0, float& a1, float& a2, f
 // (sign(b) a) / |b| -- the same correctly rounded quotient (round to nearest
 // is symmetric), and with a positive divisor the two steps keep a zero
 // numerator's sign (with a negative one +0 / b would come out +0, not -0) --
-// y = RN(1/|b|) by rcp_fast, two Markstein steps; |b| in [2^-30, 2^30) and a
+// y = RN(1/|b|) by rcp_fast, one Markstein step; |b| in [2^-30, 2^30) and a
 // zero or |a| in [2^-60, 2^60) (guarded; the IEEE division elsewhere)
 __device__ __forceinline__ float div_one(float a, float b) {
   const uint32_t ua = (__float_as_uint(a) << 1) - 1u;
