@@ -354,13 +354,36 @@ __device__ __forceinline__ double log_fast(float x) {
   return __builtin_fma((double)e, SDF_CRM_LN2, lm);
 }
 
+// Rounding v to float is safe when v's error interval [v - tol, v + tol],
+// tol = SDF_CRM_LOG_EPS |v|, holds no fp32 rounding midpoint (x a positive
+// normal float).  SDF_CRM_LOG_BITCHECK 1 (round 6) tests that on v's bits:
+// an fp32 midpoint is a double whose low 29 mantissa bits are 2^28, and tol
+// is below 2^11 of v's ulps (2^-42 |v| with |v| < 2 2^ev, ulp 2^(ev-52)), so
+// v is safe when its low 29 bits differ from 2^28 by more than 2^11 -- two
+// integer VALU on the low dword instead of an fp64 multiply, two fp64 adds
+// and two conversions (at a power of two the interval may reach the next
+// binade, whose midpoints lie 2^-25 relative away: no midpoint either).  The
+// exhaustive GPU check of all 2^32 inputs (tests/crmath "log") covers both.
+#ifndef SDF_CRM_LOG_BITCHECK
+#define SDF_CRM_LOG_BITCHECK 1
+#endif
+__device__ __forceinline__ bool log_round_ok(float x, double v, float r) {
+  const bool normal = (__float_as_uint(x) - 0x00800000u) < (0x7F800000u - 0x00800000u);
+#if SDF_CRM_LOG_BITCHECK
+  static_assert(SDF_CRM_LOG_EPS <= 0x1p-42, "tol must stay below 2^11 ulps of v");
+  (void)r;
+  const uint32_t lo = (uint32_t)__builtin_bit_cast(unsigned long long, v);
+  return normal & (((lo & 0x1FFFFFFFu) - (0x10000000u - 0x800u)) >= 0x1000u);
+#else
+  const double tol = SDF_CRM_LOG_EPS * __builtin_fabs(v);
+  return normal & ((float)(v - tol) == r) & ((float)(v + tol) == r);
+#endif
+}
+
 __device__ __forceinline__ float cr_log(float x) {
   const double v = log_fast(x);
-  // round safely: both ends of v's error interval round to the same float
-  const double tol = SDF_CRM_LOG_EPS * __builtin_fabs(v);
   const float r = (float)v;
-  const bool ok = ((float)(v - tol) == r) & ((float)(v + tol) == r) &
-                  ((__float_as_uint(x) - 0x00800000u) < (0x7F800000u - 0x00800000u));
+  const bool ok = log_round_ok(x, v, r);
   float out = r;
   if (any_lane(!ok)) {
     SDF_CRM_COLD();
@@ -370,11 +393,6 @@ __device__ __forceinline__ float cr_log(float x) {
 }
 
 // N logs behind ONE guard (as cr_sqrt_n): each out[i] == cr_log(x[i])
-__device__ __forceinline__ bool log_round_ok(float x, double v, float r) {
-  const double tol = SDF_CRM_LOG_EPS * __builtin_fabs(v);
-  return ((float)(v - tol) == r) & ((float)(v + tol) == r) &
-         ((__float_as_uint(x) - 0x00800000u) < (0x7F800000u - 0x00800000u));
-}
 template <int N>
 __device__ __forceinline__ void cr_log_n(const float (&x)[N], float (&out)[N]) {
   bool ok = true;
