@@ -43,8 +43,8 @@ enum TilesShade : uint32_t {
 // value v satisfies |v / x^n - 1| <= (n - 1) u / (1 - (n - 1) u) < 2^-46 for
 // n <= 64 (no intermediate underflows where x^n is near a float: x <= 1 keeps
 // every partial product >= x^n, x > 1 keeps it >= 1).  The exhaustive GPU
-// comparison with the library pow for every n in [0, 64]
-// (tests/test_gpu_parity.py) checks it.  Where both ends of a 2^-44 interval around it round to the same
+// comparison with the library pow for every n in [0, 64] and every x in
+// [0, 1.0001] (tests/crmath "pow", tests/test_gpu_crmath.py) checks it.  Where both ends of a 2^-44 interval around it round to the same
 // float, that float is the correct rounding of x^n -- and of the library's
 // fp64 pow, which lies in the same interval; other lanes (rounding
 // boundaries, NaN) take the library pow.  SDF_SHADE_LIBRARY_POW 1: the
@@ -59,17 +59,45 @@ __device__ __forceinline__ float spec_pow(float x, float shin) {
     const int n = (int)shin;
     if ((float)n == shin && n >= 0 && n <= 64) {
       double b = (double)x, v = 1.0;
+      // n is uniform: each step's multiplies sit behind real (scalar)
+      // branches -- an empty volatile asm keeps LLVM from if-converting them
+      // into two fp64 multiplies and four v_cndmask per step (the TILES
+      // decoder's exact shading: ~24 VALU per pixel for n = 12, 5 now)
       for (int e = n; e != 0; e >>= 1) {
-        if (e & 1) v = v * b;
-        if (e > 1) b = b * b;
+        if (e & 1) {
+#if !defined(SDF_SHADE_POW_BRANCH) || SDF_SHADE_POW_BRANCH
+          asm volatile("");
+#endif
+          v = v * b;
+        }
+        if (e > 1) {
+#if !defined(SDF_SHADE_POW_BRANCH) || SDF_SHADE_POW_BRANCH
+          asm volatile("");
+#endif
+          b = b * b;
+        }
       }
-      const double tol = 0x1p-44 * __builtin_fabs(v);
       const float r = (float)v;
-      const bool ok = ((float)(v - tol) == r) & ((float)(v + tol) == r);
+#if !defined(SDF_SHADE_POW_BITCHECK) || SDF_SHADE_POW_BITCHECK
+      // The same test on v's bits (as cr_math.h log_round_ok): for a normal
+      // float r, an fp32 rounding midpoint is a double with low 29 mantissa
+      // bits 2^28, and the tolerance is below 2^9 of v's ulps; v < 2^-151
+      // rounds to +0 from anywhere in its interval.  Lanes with a subnormal
+      // r (x^n in [2^-151, 2^-126): x^12 for x in ~[1.6e-4, 6.9e-4]) take
+      // the interval test below, the library pow only where that fails.
+      const uint32_t lo = (uint32_t)__builtin_bit_cast(unsigned long long, v);
+      const bool ok = ((((lo & 0x1FFFFFFFu) - (0x10000000u - 0x200u)) >= 0x400u) &
+                       (r >= 0x1p-126f)) | (v < 0x1p-151);
+#else
+      const double tol0 = 0x1p-44 * __builtin_fabs(v);
+      const bool ok = ((float)(v - tol0) == r) & ((float)(v + tol0) == r);
+#endif
       float out = r;
       if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
         asm volatile("" ::: "memory");   // keep the library pow out of the fast path
-        out = ok ? r : (float)pow((double)x, (double)shin);
+        const double tol = 0x1p-44 * __builtin_fabs(v);
+        const bool ok2 = ok | (((float)(v - tol) == r) & ((float)(v + tol) == r));
+        out = ok2 ? r : (float)pow((double)x, (double)shin);
       }
       return out;
     }
