@@ -321,6 +321,17 @@ __device__ __forceinline__ double fma64(double p, double s, double c) {
 #endif
 }
 
+// The library fp64 log (the oracle's reading), out of line: only the rare
+// lanes near a rounding boundary call it, and its constants stay out of the
+// callers' loops (shade.h library_pow)
+#if !defined(SDF_CRM_LOG_CALL) || SDF_CRM_LOG_CALL
+inline __device__ __attribute__((noinline)) float library_log(float x) {
+  return (float)log((double)x);
+}
+#else
+__device__ __forceinline__ float library_log(float x) { return (float)log((double)x); }
+#endif
+
 __device__ __forceinline__ double log_fast(float x) {
   // x = 2^e m, m in [sqrt(1/2), sqrt(2))
   float mf = __builtin_amdgcn_frexp_mantf(x);            // [0.5, 1)
@@ -387,7 +398,7 @@ __device__ __forceinline__ float cr_log(float x) {
   float out = r;
   if (any_lane(!ok)) {
     SDF_CRM_COLD();
-    out = ok ? r : (float)log((double)x);
+    out = ok ? r : library_log(x);
   }
   return out;
 }
@@ -407,7 +418,7 @@ __device__ __forceinline__ void cr_log_n(const float (&x)[N], float (&out)[N]) {
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const double v = log_fast(x[i]);
-      if (!log_round_ok(x[i], v, out[i])) out[i] = (float)log((double)x[i]);
+      if (!log_round_ok(x[i], v, out[i])) out[i] = library_log(x[i]);
     }
   }
 }

@@ -51,6 +51,20 @@ enum TilesShade : uint32_t {
 // library pow alone -- the same floats (the TILES decoder used it until
 // round 5 to keep its tile loop rolled at 8 waves/SIMD; on exact-precision
 // streams it cost 0.084 ms of decode per 4K frame, tiles.hip).
+// The library fp64 pow, out of line (SDF_SHADE_POW_CALL 1): inlined, its
+// ~30 fp64 constants were hoisted out of the persistent frames kernel's tile
+// loop (render_kernel.inc render_frames) and spilled to scratch; as a call
+// they exist only on the rare lanes that need it.
+#if !defined(SDF_SHADE_POW_CALL) || SDF_SHADE_POW_CALL
+inline __device__ __attribute__((noinline)) float library_pow(float x, float y) {
+  return (float)pow((double)x, (double)y);
+}
+#else
+__device__ __forceinline__ float library_pow(float x, float y) {
+  return (float)pow((double)x, (double)y);
+}
+#endif
+
 template <bool EXACT>
 __device__ __forceinline__ float spec_pow(float x, float shin) {
 #pragma clang fp contract(off)
@@ -97,12 +111,12 @@ __device__ __forceinline__ float spec_pow(float x, float shin) {
         asm volatile("" ::: "memory");   // keep the library pow out of the fast path
         const double tol = 0x1p-44 * __builtin_fabs(v);
         const bool ok2 = ok | (((float)(v - tol) == r) & ((float)(v + tol) == r));
-        out = ok2 ? r : (float)pow((double)x, (double)shin);
+        out = ok2 ? r : library_pow(x, shin);
       }
       return out;
     }
 #endif
-    return (float)pow((double)x, (double)shin);
+    return library_pow(x, shin);
   } else {
     return __builtin_amdgcn_exp2f(shin * __builtin_amdgcn_logf(x));
   }

@@ -27,12 +27,15 @@ def main():
     ap.add_argument("--precision", default="exact")
     ap.add_argument("--calls", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="another libsdf3d.so build (A/B)")
     ap.add_argument("--period", type=int, default=16,
                     help="the schedule measures block costs every `period` launches")
     a = ap.parse_args()
     import torch
     from sdf3d_amd import Renderer, abi, scenes
     rd = Renderer("cuda:0")
+    if a.lib:
+        rd.lib = abi.load_library(a.lib, any_version=True)
     f = scenes.config(a.config, precision=abi.PRECISION_EXACT if a.precision == "exact"
                       else abi.PRECISION_FAST)
     out = rd.alloc(f)[0]
@@ -65,6 +68,7 @@ def main():
     same = bool(torch.equal(out.view(torch.int32), out2.view(torch.int32)))
     same3 = bool(torch.equal(out.view(torch.int32), out3.view(torch.int32)))
     print(json.dumps({"config": a.config, "precision": a.precision, "calls": a.calls,
+                      "lib": a.lib or "tree",
                       **{k + "_ms": round(statistics.median(v), 4) for k, v in res.items()},
                       "frames1_bit_exact": same, "scheduled_bit_exact": same3,
                       "schedule_period": a.period}), flush=True)
