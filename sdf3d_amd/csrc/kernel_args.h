@@ -135,8 +135,12 @@ static_assert(sizeof(RenderArgs) <= 4096, "RenderArgs exceeds the 4 KiB kernel-a
 // Tiles a wave takes per queue request, queues per launch (workgroup b uses
 // queue b % queues, i.e. one per XCD), and the queues' spacing in uint32s:
 // requests on one address serialise at the memory-side atomic unit, so the
-// launch spreads them over several addresses and asks for 2 tiles at a time.
-constexpr int kChunkTiles = 2;
+// launch spreads them over several addresses.  One tile per request since
+// round 6: the same rate on 16-frame launches (r02 sweep: 0.3665 against
+// 0.3663 ms per frame with 2), and a ONE-frame launch 0.384 -> 0.237 ms on
+// C3 exact, where larger requests leave waves without tiles (a 1080p frame
+// has ~4 tiles per wave; profiles/r06_frames1_env.jsonl).
+constexpr int kChunkTiles = 1;
 constexpr int kFrameQueues = 32;   // at most; kDefaultQueues by default
 constexpr int kDefaultQueues = 8;
 constexpr int kQueueStride = 64;

@@ -34,7 +34,7 @@ SETS = [
 
 def run_set(cmd, counters, outdir: Path, kernel: str):
     d = outdir / ("pmc_" + "_".join(c.lower() for c in counters)[:48])
-    full = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o",
+    full = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o",
             "run", "--", *cmd]
     r = subprocess.run(full, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
@@ -73,6 +73,12 @@ def main():
     out["valu_per_wave"] = round(res.get("SQ_INSTS_VALU", 0) / w, 1)
     out["lds_per_wave"] = round(res.get("SQ_INSTS_LDS", 0) / w, 1)
     out["smem_per_wave"] = round(res.get("SQ_INSTS_SMEM", 0) / w, 1)
+    calib = Path(__file__).resolve().parent.parent / "profiles" / "r02_valu_busy_calib.json"
+    if res.get("SQ_ACTIVE_INST_VALU") and res.get("GRBM_GUI_ACTIVE") and calib.exists():
+        # tools/pmc_traffic.py's calibrated form (a lower bound)
+        cpu = json.loads(calib.read_text())["cycles_per_unit"]
+        out["valu_busy_calibrated"] = round(
+            cpu * res["SQ_ACTIVE_INST_VALU"] / (1024 * res["GRBM_GUI_ACTIVE"] / 8), 4)
     if "TCC_EA0_WRREQ_sum" in res:
         out["write_bytes"] = res["TCC_EA0_WRREQ_sum"] * 64
         out["fetch_bytes"] = res["TCC_EA0_RDREQ_sum"] * 64 * 2

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--calls", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--lib", default=None, help="another libsdf3d.so build (A/B)")
+    ap.add_argument("--only", default=None, choices=["render", "frames1", "scheduled"],
+                    help="run one leg only (for rocprofv3 counter passes)")
     ap.add_argument("--period", type=int, default=16,
                     help="the schedule measures block costs every `period` launches")
     a = ap.parse_args()
@@ -60,11 +62,17 @@ def main():
     legs = {"render": lambda: rd.render(f, out=out, stream=s),
             "frames1": lambda: rd.render_frames(f, [f.camera], [out2], stream=s),
             "scheduled": lambda: rd.render(f, out=out3, stream=s, schedule=sch)}
+    if a.only:
+        legs = {a.only: legs[a.only]}
     res = {k: [] for k in legs}
     for _ in range(a.rounds):
         for k, fn in legs.items():
             res[k].append(timed(fn))
     torch.cuda.synchronize()
+    if a.only:
+        print(json.dumps({"config": a.config, "precision": a.precision, "only": a.only,
+                          a.only + "_ms": round(statistics.median(res[a.only]), 4)}), flush=True)
+        return
     same = bool(torch.equal(out.view(torch.int32), out2.view(torch.int32)))
     same3 = bool(torch.equal(out.view(torch.int32), out3.view(torch.int32)))
     print(json.dumps({"config": a.config, "precision": a.precision, "calls": a.calls,
