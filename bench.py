@@ -64,8 +64,11 @@ def _gloo_rehearsal(argv):
                for i, a in enumerate(argv))
 
 
+# At N > 1 up to 8 render streams plus 2 communication streams (the
+# Mandelbulb's 8 buffer sets, below): 12 queues (the pool allows up to 32).
 if not _gloo_rehearsal(sys.argv[1:]):
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES",
+                          "12" if int(os.environ.get("WORLD_SIZE", "1")) > 1 else "8")
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mpixels/s (primary+shadow+AO) at 3840×2160, 1/2/4/8 MI355X"
@@ -102,7 +105,7 @@ def parse():
                     help="render streams / buffer sets of the frame driver (frame i on "
                          "stream i %% streams: a frame starts while the previous one's "
                          "slowest tiles finish); 1 serialises launches (profiling); "
-                         "0 = 3 at N=1, 4 at N>1")
+                         "0 = 3 at N=1; at N>1 4, 8 for the Mandelbulb")
     ap.add_argument("--lag", type=int, default=2,
                     help="N>1: frames between a batch's last render and its gather (the "
                          "host reads the batch's agreed stream lengths that much later)")
@@ -388,7 +391,13 @@ def main():
     t = R.tiling(rank, world, 8, shares=shares)
     t_equal = R.tiling(rank, world, 8)
     rows = R.owned_rows(H, t)
-    nbuf = args.streams or (3 if world == 1 else 4)
+    # N > 1: a peer's share of the Mandelbulb (1/7 of the rows, 8-row blocks
+    # interleaved) runs short kernels with long tails, and more frames in
+    # flight fill them: its TILES share 0.154 / 0.123 / 0.113 / 0.110 ms on
+    # 3 / 4 / 6 / 8 streams, where C4's is best at 4 (0.0668 against 0.0683
+    # on 8; profiles/r06_peer_streams.jsonl)
+    bulb = frame.scene.kind == abi.SCENE_MANDELBULB
+    nbuf = args.streams or (3 if world == 1 else (8 if bulb else 4))
     batch = (args.batch or 2) if world > 1 else 1
     if nbuf % batch:
         batch = 1
