@@ -84,8 +84,18 @@ def instrument(lines: list[str], kernel: str, frame_off: int, rgba_karg: int):
     returns (new lines, blocks: list of {id, label, ins: [(op, text, idx)]})."""
     # spare VGPRs above the kernel's own (its .num_vgpr), 8 of them
     global SPARE, NEXT_FREE
-    nv = next(int(m.group(1)) for l in lines
-              for m in [re.match(rf"\s*\.set {re.escape(kernel)}\.num_vgpr, (\d+)", l)] if m)
+    # ".set K.num_vgpr, N", or "max(N, .Lcallee.num_vgpr, ...)" when the kernel
+    # makes calls (the library log/pow fall-backs): the largest of them
+    sets = {m.group(1): m.group(2) for l in lines
+            for m in [re.match(r"\s*\.set (\S+)\.num_vgpr, (.+)$", l)] if m}
+
+    def num_vgpr(sym, depth=0):
+        rhs = sets[sym]
+        vals = [int(x) for x in re.findall(r"(?<![\w.])(\d+)(?![\w.])", rhs)]
+        vals += [num_vgpr(c, depth + 1) for c in re.findall(r"(\.?[\w.]+?)\.num_vgpr", rhs)
+                 if depth < 4 and c in sets]
+        return max(vals)
+    nv = num_vgpr(kernel)
     SPARE = (nv + 3) // 4 * 4
     NEXT_FREE = SPARE + 8
     start = next(i for i, l in enumerate(lines) if re.match(rf"^{re.escape(kernel)}:", l))
@@ -285,9 +295,16 @@ def cmd_build(a):
         e = next(i for i in range(s, len(lines)) if lines[i].startswith(".Lfunc_end"))
         return [l.split(";")[0].strip() for l in lines[s:e]
                 if l.startswith("\t") and l.strip() and not l.strip().startswith((".", ";"))]
-    same = stream(orig) == stream(prod.read_text().split("\n"))
-    print(f"kernel {kname}: -gline-tables-only stream identical to production: {same}")
-    if not same:
+    so, sp = stream(orig), stream(prod.read_text().split("\n"))
+    same = so == sp
+    # the same instructions up to register numbering (the register allocator
+    # may number differently with line tables): the block structure, every
+    # opcode and every non-register operand equal -- the counts are exact
+    reg = re.compile(r"\b[vsa]\[\d+:\d+\]|\b[vsa]\d+\b")
+    same_ops = len(so) == len(sp) and all(reg.sub("R", x) == reg.sub("R", y) for x, y in zip(so, sp))
+    print(f"kernel {kname}: -gline-tables-only stream identical to production: {same}"
+          f" (up to register numbering: {same_ops})")
+    if not same_ops:
         raise SystemExit("debug line tables changed the code: attribution would not be exact")
     # the un-instrumented code object (symbolization)
     asm_i = next(i for i, c in enumerate(cmds) if "-cc1as" in c and "amdgcn-amd-amdhsa" in c)

@@ -37,6 +37,7 @@ def build() -> Path:
 
 def write_frame(path: Path, cfg: str, world: int, a: int, b: int, sets: int,
                 precision: str = "fast") -> None:
+    import numpy as np
     from sdf3d_amd import abi, scenes
     prec = abi.PRECISION_FAST if precision == "fast" else abi.PRECISION_EXACT
     f = scenes.config(cfg, precision=prec)
@@ -44,8 +45,10 @@ def write_frame(path: Path, cfg: str, world: int, a: int, b: int, sets: int,
     for s in range(sets):
         g = scenes.config(cfg, precision=prec, pose=s % len(scenes.POSES))
         if s >= len(scenes.POSES):   # more sets than poses: small extra yaw
-            scenes.set_view(g, scenes.orbit_view(*scenes.POSES[s % len(scenes.POSES)])
-                            @ scenes.orbit_view(3.0 * (s // len(scenes.POSES)), 0.0))
+            m = lambda v: np.asarray(v, dtype=np.float64).reshape(4, 4, order="F")  # noqa: E731
+            v = m(scenes.orbit_view(*scenes.POSES[s % len(scenes.POSES)])) @ m(
+                scenes.orbit_view(3.0 * (s // len(scenes.POSES)), 0.0))
+            scenes.set_view(g, v.astype(np.float32).reshape(16, order="F"))
         cams.append(bytes(g.camera))
     blob = (bytes(f.scene) + bytes(f.light) + bytes(f.material) + bytes(f.params)
             + bytes((C.c_int32 * 4)(world, a, b, sets)) + b"".join(cams))
