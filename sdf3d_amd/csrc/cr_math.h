@@ -197,12 +197,25 @@ __device__ __forceinline__ bool div3_ok(float a0, float a1, float a2, float l) {
 }
 // (a0, a1, a2) / l from the host's y = RN(1/l), l's range checked by the
 // caller (wave-uniform): the Mandelbulb's (p - c) / scale
+// SDF_CRM_DIV3_MIN3 1 (round 6): the wave's fast test is ONE v_min3_f32 of
+// the numerators' magnitudes against 2^-60 (2 VALU instead of 5); a wave
+// where it fails (a zero numerator: the Mandelbulb's p - c is rarely exactly
+// zero) takes the exact numerators_ok test in the cold block.  Same
+// quotients: a lane passing the min3 test passes numerators_ok.
+#ifndef SDF_CRM_DIV3_MIN3
+#define SDF_CRM_DIV3_MIN3 1
+#endif
 __device__ __forceinline__ void div3_prepared(float& a0, float& a1, float& a2, float l, float y) {
-  const bool ok = numerators_ok(a0, a1, a2);
+#if SDF_CRM_DIV3_MIN3
+  const bool fast = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a0), __builtin_fabsf(a1)),
+                                    __builtin_fabsf(a2)) >= 0x1p-60f;
+#else
+  const bool fast = numerators_ok(a0, a1, a2);
+#endif
   float q0 = div_refined(a0, l, y), q1 = div_refined(a1, l, y), q2 = div_refined(a2, l, y);
-  if (any_lane(!ok)) {
+  if (any_lane(!fast)) {
     SDF_CRM_COLD();
-    if (!ok) {
+    if (!numerators_ok(a0, a1, a2)) {
       q0 = a0 / l;
       q1 = a1 / l;
       q2 = a2 / l;
