@@ -120,10 +120,11 @@ def test_rcp_fast_negative_half(results):
 
 def test_markstein_divisions_are_ieee(results):
     """normalize / the Mandelbulb's divisions / the shadow march's division
-    by one reciprocal and two Markstein steps (cr_math.h div_one,
-    div_refined): bit-identical to IEEE a / b on 2^32 sampled pairs, inside
-    the guard by the two steps themselves ("effective" 0), everywhere with the
-    guard's fall-back ("mismatch" 0)."""
+    by one reciprocal and one Markstein step (cr_math.h div_one,
+    div_refined; round 6, proof in cr_math.h and tests/test_crmath_host.py):
+    bit-identical to IEEE a / b on 2^32 sampled pairs, inside the guard by
+    the step itself ("effective" 0), everywhere with the guard's fall-back
+    ("mismatch" 0)."""
     r = results["div"]
     assert r["inputs"] == 2**32 and r["mismatch"] == 0 and r["effective"] == 0, r
     assert r["fast_path"] > 0.7 * 2**32, r
