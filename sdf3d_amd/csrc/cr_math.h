@@ -227,7 +227,7 @@ __device__ __forceinline__ void div3_prepared(float& a0, float& a1, float& a2, f
 }
 // a / b for one division (the DE's, the shadow march's): computed as
 // (sign(b) a) / |b| -- the same correctly rounded quotient (round to nearest
-// is symmetric), and with a positive divisor the step keeps a zero
+// is symmetric), and with a positive divisor the two steps keep a zero
 // numerator's sign (with a negative one +0 / b would come out +0, not -0) --
 // y = RN(1/|b|) by rcp_fast, one Markstein step; |b| in [2^-30, 2^30) and a
 // zero or |a| in [2^-60, 2^60) (guarded; the IEEE division elsewhere)
